@@ -1,0 +1,310 @@
+// G1 (y^2 = x^3 + 4 over Fp) and G2 (y^2 = x^3 + 4(1+u) over Fp2).
+//
+// Homogeneous projective coordinates with the complete a = 0 formulas of
+// Renes-Costello-Batina (eprint 2015/1060, Alg. 7/8/9): exact on every input,
+// including small-order points crafted by an adversary, which matters because
+// subgroup checks run on attacker-chosen encodings.
+//
+// Reference call sites replaced (bls12_381 0.7.1):
+//   G1Affine::from_compressed   utils/verify-bls-signatures/src/lib.rs:144
+//   G2Affine::from_compressed   utils/verify-bls-signatures/src/lib.rs:74
+//   to_compressed               src/lib.rs:64, :134
+//   is_torsion_free (G1: phi(P) == -[x^2]P, G2: psi(P) == [x]P; eprint 2021/1130, 2022/352)
+#pragma once
+#include "field.hpp"
+
+namespace bls {
+
+template <class F>
+struct proj {
+  F x, y, z;
+};
+template <class F>
+struct affine {
+  F x, y;
+  bool inf;
+};
+using g1p = proj<fp>;
+using g2p = proj<fp2>;
+using g1a = affine<fp>;
+using g2a = affine<fp2>;
+
+CESS_HD fp mul_b3(const fp& a) { return mul4(mul3(a)); }             // * 12
+CESS_HD fp2 mul_b3(const fp2& a) { return mul4(mul3(mul_nr(a))); }   // * 12(1+u)
+template <class F> CESS_HD F f_zero();
+template <> CESS_HD fp f_zero<fp>() { return fp_zero(); }
+template <> CESS_HD fp2 f_zero<fp2>() { return fp2_zero(); }
+template <class F> CESS_HD F f_one();
+template <> CESS_HD fp f_one<fp>() { return fp_one(); }
+template <> CESS_HD fp2 f_one<fp2>() { return fp2_one(); }
+
+template <class F>
+CESS_HD proj<F> proj_identity() {
+  return {f_zero<F>(), f_one<F>(), f_zero<F>()};
+}
+template <class F>
+CESS_HD proj<F> proj_from_affine(const affine<F>& a) {
+  if (a.inf) return proj_identity<F>();
+  return {a.x, a.y, f_one<F>()};
+}
+
+// RCB Alg. 9 (doubling, a = 0)
+template <class F>
+CESS_HD proj<F> proj_dbl(const proj<F>& p) {
+  F t0 = sqr(p.y);
+  F z3 = mul8(t0);
+  F t1 = mul(p.y, p.z);
+  F t2 = sqr(p.z);
+  t2 = mul_b3(t2);
+  F x3 = mul(t2, z3);
+  F y3 = add(t0, t2);
+  z3 = mul(t1, z3);
+  t1 = dbl(t2);
+  t2 = add(t1, t2);
+  t0 = sub(t0, t2);
+  y3 = mul(t0, y3);
+  y3 = add(x3, y3);
+  t1 = mul(p.x, p.y);
+  x3 = mul(t0, t1);
+  x3 = dbl(x3);
+  return {x3, y3, z3};
+}
+
+// RCB Alg. 7 (addition, a = 0)
+template <class F>
+CESS_HD proj<F> proj_add(const proj<F>& p, const proj<F>& q) {
+  F t0 = mul(p.x, q.x);
+  F t1 = mul(p.y, q.y);
+  F t2 = mul(p.z, q.z);
+  F t3 = mul(add(p.x, p.y), add(q.x, q.y));
+  F t4 = add(t0, t1);
+  t3 = sub(t3, t4);
+  t4 = mul(add(p.y, p.z), add(q.y, q.z));
+  F x3 = add(t1, t2);
+  t4 = sub(t4, x3);
+  x3 = mul(add(p.x, p.z), add(q.x, q.z));
+  F y3 = add(t0, t2);
+  y3 = sub(x3, y3);
+  x3 = dbl(t0);
+  t0 = add(x3, t0);
+  t2 = mul_b3(t2);
+  F z3 = add(t1, t2);
+  t1 = sub(t1, t2);
+  y3 = mul_b3(y3);
+  x3 = mul(t4, y3);
+  t2 = mul(t3, t1);
+  x3 = sub(t2, x3);
+  y3 = mul(y3, t0);
+  t1 = mul(t1, z3);
+  y3 = add(t1, y3);
+  t0 = mul(t0, t3);
+  z3 = mul(z3, t4);
+  z3 = add(z3, t0);
+  return {x3, y3, z3};
+}
+
+// RCB Alg. 8 (mixed addition, q affine and not the identity)
+template <class F>
+CESS_HD proj<F> proj_add_mixed(const proj<F>& p, const F& qx, const F& qy) {
+  F t0 = mul(p.x, qx);
+  F t1 = mul(p.y, qy);
+  F t3 = mul(add(qx, qy), add(p.x, p.y));
+  F t4 = add(t0, t1);
+  t3 = sub(t3, t4);
+  t4 = add(mul(qy, p.z), p.y);
+  F y3 = add(mul(qx, p.z), p.x);
+  F x3 = dbl(t0);
+  t0 = add(x3, t0);
+  F t2 = mul_b3(p.z);
+  F z3 = add(t1, t2);
+  t1 = sub(t1, t2);
+  y3 = mul_b3(y3);
+  x3 = mul(t4, y3);
+  t2 = mul(t3, t1);
+  x3 = sub(t2, x3);
+  y3 = mul(y3, t0);
+  t1 = mul(t1, z3);
+  y3 = add(t1, y3);
+  t0 = mul(t0, t3);
+  z3 = mul(z3, t4);
+  z3 = add(z3, t0);
+  return {x3, y3, z3};
+}
+
+template <class F>
+CESS_HD proj<F> proj_neg(const proj<F>& p) {
+  return {p.x, neg(p.y), p.z};
+}
+template <class F>
+CESS_HD bool proj_is_identity(const proj<F>& p) {
+  return is_zero(p.z);
+}
+// projective equality (both may be the identity)
+template <class F>
+CESS_HD bool proj_eq(const proj<F>& p, const proj<F>& q) {
+  bool pi = is_zero(p.z), qi = is_zero(q.z);
+  if (pi || qi) return pi && qi;
+  return eq(mul(p.x, q.z), mul(q.x, p.z)) && eq(mul(p.y, q.z), mul(q.y, p.z));
+}
+template <class F>
+CESS_HD affine<F> proj_to_affine(const proj<F>& p) {
+  affine<F> r;
+  r.inf = is_zero(p.z);
+  F zi = inv(p.z);
+  r.x = mul(p.x, zi);
+  r.y = mul(p.y, zi);
+  if (r.inf) {
+    r.x = f_zero<F>();
+    r.y = f_one<F>();
+  }
+  return r;
+}
+
+// [k]P for a fixed 64-bit scalar k (MSB first, complete formulas)
+template <class F>
+CESS_HD proj<F> proj_mul_u64(const proj<F>& p, uint64_t k) {
+  proj<F> acc = proj_identity<F>();
+  bool started = false;
+  for (int b = 63; b >= 0; b--) {
+    if (started) acc = proj_dbl(acc);
+    if ((k >> b) & 1u) {
+      acc = started ? proj_add(acc, p) : p;
+      started = true;
+    }
+  }
+  return acc;
+}
+template <class F>
+CESS_HD proj<F> proj_mul_u64_mixed(const F& px, const F& py, uint64_t k) {
+  proj<F> acc = proj_identity<F>();
+  bool started = false;
+  for (int b = 63; b >= 0; b--) {
+    if (started) acc = proj_dbl(acc);
+    if ((k >> b) & 1u) {
+      acc = started ? proj_add_mixed(acc, px, py) : proj<F>{px, py, f_one<F>()};
+      started = true;
+    }
+  }
+  return acc;
+}
+
+constexpr uint64_t BLS_X_ABS = 0xd201000000010000ull;   // x = -BLS_X_ABS
+constexpr uint64_t H_EFF_G1 = 0xd201000000010001ull;    // 1 - x
+
+// [k]P for a 256-bit scalar (little-endian 8 words), used by keygen/sign
+template <class F>
+CESS_HD proj<F> proj_mul_scalar_mixed(const F& px, const F& py, const uint32_t (&k)[8]) {
+  proj<F> acc = proj_identity<F>();
+  for (int w = 7; w >= 0; w--) {
+    for (int b = 31; b >= 0; b--) {
+      acc = proj_dbl(acc);
+      if ((k[w] >> b) & 1u) acc = proj_add_mixed(acc, px, py);
+    }
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// subgroup checks
+// ---------------------------------------------------------------------------
+// G1: phi(P) == -[x^2]P  with phi(x, y) = (beta x, y)   (P affine, not identity)
+CESS_HD bool g1_is_torsion_free(const fp& px, const fp& py) {
+  g1p xp = proj_mul_u64_mixed(px, py, BLS_X_ABS);   // [|x|]P
+  g1p x2p = proj_mul_u64(xp, BLS_X_ABS);           // [x^2]P
+  g1p phi = {mul(px, fp_from(c::G1_BETA)), py, fp_one()};
+  return proj_eq(phi, proj_neg(x2p));
+}
+// G2: psi(P) == [x]P = -[|x|]P
+CESS_HD fp2 psi_x_coeff() { return {fp_from(c::PSI_X_C0), fp_from(c::PSI_X_C1)}; }
+CESS_HD fp2 psi_y_coeff() { return {fp_from(c::PSI_Y_C0), fp_from(c::PSI_Y_C1)}; }
+CESS_HD bool g2_is_torsion_free(const fp2& px, const fp2& py) {
+  g2p xp = proj_mul_u64_mixed(px, py, BLS_X_ABS);
+  g2p psi = {mul(conj(px), psi_x_coeff()), mul(conj(py), psi_y_coeff()), fp2_one()};
+  return proj_eq(psi, proj_neg(xp));
+}
+
+// ---------------------------------------------------------------------------
+// ZCash compressed encodings
+// ---------------------------------------------------------------------------
+// Inputs are the encodings as big-endian 32-bit words (w[0] = bytes 0..3).
+CESS_HD fp raw_from_be_words(const uint32_t* w) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = w[11 - i];
+  return r;
+}
+
+// returns true if valid; out.inf set for the identity encoding
+CESS_HD bool g1_decompress(const uint32_t* w, g1a& out) {
+  uint32_t flags = w[0] >> 29;
+  bool cflag = flags & 4, iflag = flags & 2, sflag = flags & 1;
+  fp xr = raw_from_be_words(w);
+  xr.v[11] &= 0x1fffffffu;
+  out.inf = false;
+  out.x = fp_zero();
+  out.y = fp_one();
+  if (!raw_lt_p(xr)) return false;
+  if (iflag && cflag && !sflag && is_zero(xr)) {
+    out.inf = true;
+    return true;
+  }
+  if (iflag || !cflag) return false;   // (any such encoding is InvalidPoint)
+  fp x = to_mont(xr);
+  fp y;
+  if (!sqrt(y, add(mul(sqr(x), x), fp_from(c::B1)))) return false;
+  if (lex_largest(y) != sflag) y = neg(y);
+  if (!g1_is_torsion_free(x, y)) return false;
+  out.x = x;
+  out.y = y;
+  return true;
+}
+
+CESS_HD bool g2_decompress(const uint32_t* w, g2a& out) {
+  uint32_t flags = w[0] >> 29;
+  bool cflag = flags & 4, iflag = flags & 2, sflag = flags & 1;
+  fp x1r = raw_from_be_words(w);
+  x1r.v[11] &= 0x1fffffffu;
+  fp x0r = raw_from_be_words(w + 12);
+  out.inf = false;
+  out.x = fp2_zero();
+  out.y = fp2_one();
+  if (!raw_lt_p(x1r) || !raw_lt_p(x0r)) return false;
+  if (iflag && cflag && !sflag && is_zero(x1r) && is_zero(x0r)) {
+    out.inf = true;
+    return true;
+  }
+  if (iflag || !cflag) return false;
+  fp2 x = {to_mont(x0r), to_mont(x1r)};
+  fp2 b2 = {fp_from(c::B1), fp_from(c::B1)};   // 4(1 + u)
+  fp2 y;
+  if (!sqrt(y, add(mul(sqr(x), x), b2))) return false;
+  if (lex_largest(y) != sflag) y = neg(y);
+  if (!g2_is_torsion_free(x, y)) return false;
+  out.x = x;
+  out.y = y;
+  return true;
+}
+
+CESS_HD void g1_compress(const g1a& p, uint8_t* out) {
+  if (p.inf) {
+    for (int i = 0; i < 48; i++) out[i] = 0;
+    out[0] = 0xc0;
+    return;
+  }
+  raw_to_be48(from_mont(p.x), out);
+  out[0] |= 0x80;
+  if (lex_largest(p.y)) out[0] |= 0x20;
+}
+CESS_HD void g2_compress(const g2a& p, uint8_t* out) {
+  if (p.inf) {
+    for (int i = 0; i < 96; i++) out[i] = 0;
+    out[0] = 0xc0;
+    return;
+  }
+  raw_to_be48(from_mont(p.x.c1), out);
+  raw_to_be48(from_mont(p.x.c0), out + 48);
+  out[0] |= 0x80;
+  if (lex_largest(p.y)) out[0] |= 0x20;
+}
+
+}  // namespace bls

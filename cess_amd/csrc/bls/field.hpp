@@ -1,0 +1,527 @@
+// BLS12-381 field tower for CDNA4 (gfx950): Fp, Fp2, Fp6, Fp12.
+//
+// Representation: 12 x u32 little-endian limbs, Montgomery form with R = 2^384,
+// every value fully reduced (< p) after every operation.
+//
+// Hot primitive: product-scanning (Comba) Montgomery multiplication with a
+// 96-bit column accumulator.  One limb product = one `v_mad_u64_u32` (64-bit
+// addend, carry-out to an SGPR pair) + one `v_addc_co_u32` into the third word:
+// 288 mads per Fp multiply (144 for a*b, 144 for m*p).
+//
+// Replaces the arithmetic of the `bls12_381` 0.7.1 crate (Fp/Fp2/Fp6/Fp12) that
+// the reference calls from utils/verify-bls-signatures/src/lib.rs:14-16.
+//
+// The same source compiles for the host only inside the test harness
+// (tests/hostemu, macro CESS_HOSTEMU) so that the device algorithms can be
+// checked against the oracle on a machine without a GPU; the product library
+// is built for gfx950 only.
+#pragma once
+#include <stdint.h>
+
+#if defined(CESS_HOSTEMU)
+#define CESS_HD inline
+#define CESS_CONST static constexpr
+#else
+#include <hip/hip_runtime.h>
+#define CESS_HD __device__ __forceinline__
+#define CESS_CONST static constexpr
+#endif
+
+#include "consts.hpp"
+
+namespace bls {
+
+// ---------------------------------------------------------------------------
+// 96-bit multiply-accumulate: (hi:acc) += a * b
+// ---------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+CESS_HD void mac(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& hi) {
+  uint64_t c, d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "v"(b));
+  asm("v_addc_co_u32 %0, %1, %0, 0, %2" : "+v"(hi), "=s"(d) : "s"(c));
+}
+// b is wave-uniform (a constant): keep it in an SGPR
+CESS_HD void mac_k(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& hi) {
+  uint64_t c, d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "s"(b));
+  asm("v_addc_co_u32 %0, %1, %0, 0, %2" : "+v"(hi), "=s"(d) : "s"(c));
+}
+#else
+CESS_HD void mac(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& hi) {
+  uint64_t s = (uint64_t)a * b + acc;
+  hi += (s < acc);
+  acc = s;
+}
+CESS_HD void mac_k(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& hi) { mac(a, b, acc, hi); }
+#endif
+
+struct fp {
+  uint32_t v[12];
+};
+struct fp2 {
+  fp c0, c1;
+};
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+// ---------------------------------------------------------------------------
+// Fp
+// ---------------------------------------------------------------------------
+CESS_HD fp fp_from(const uint32_t (&k)[12]) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = k[i];
+  return r;
+}
+CESS_HD fp fp_zero() {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = 0;
+  return r;
+}
+CESS_HD fp fp_one() { return fp_from(c::ONE); }
+
+// r = t - p if t >= p  (t < 2p)
+CESS_HD fp fp_reduce_once(const fp& t) {
+  fp s;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t d = (uint64_t)t.v[i] - c::P_RAW[i] - borrow;
+    s.v[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = borrow ? t.v[i] : s.v[i];
+  return r;
+}
+
+CESS_HD fp add(const fp& a, const fp& b) {
+  fp t;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t s = (uint64_t)a.v[i] + b.v[i] + carry;
+    t.v[i] = (uint32_t)s;
+    carry = (uint32_t)(s >> 32);
+  }
+  return fp_reduce_once(t);  // a + b < 2p < 2^382: no carry out of limb 11
+}
+
+CESS_HD fp sub(const fp& a, const fp& b) {
+  fp t;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
+    t.v[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  // if borrow: add p back
+  uint32_t mask = 0u - borrow;
+  uint32_t carry = 0;
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t s = (uint64_t)t.v[i] + (c::P_RAW[i] & mask) + carry;
+    r.v[i] = (uint32_t)s;
+    carry = (uint32_t)(s >> 32);
+  }
+  return r;
+}
+
+CESS_HD fp dbl(const fp& a) { return add(a, a); }
+
+CESS_HD bool is_zero(const fp& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) acc |= a.v[i];
+  return acc == 0;
+}
+
+CESS_HD fp neg(const fp& a) {
+  // p - a, and 0 -> 0
+  fp r;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t d = (uint64_t)c::P_RAW[i] - a.v[i] - borrow;
+    r.v[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  bool z = is_zero(a);
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = z ? 0u : r.v[i];
+  return r;
+}
+
+CESS_HD bool eq(const fp& a, const fp& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+CESS_HD fp select(bool c, const fp& a, const fp& b) {  // c ? a : b
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// Montgomery product a*b*R^-1 mod p (product scanning, interleaved reduction)
+CESS_HD fp mul(const fp& a, const fp& b) {
+  uint32_t m[12];
+  fp t;
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) mac(a.v[i], b.v[k - i], acc, hi);
+#pragma unroll
+    for (int i = 0; i < k; i++) mac_k(m[i], c::P_RAW[k - i], acc, hi);
+    m[k] = (uint32_t)acc * c::PINV;
+    mac_k(m[k], c::P_RAW[0], acc, hi);
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 12; k < 23; k++) {
+#pragma unroll
+    for (int i = k - 11; i < 12; i++) {
+      mac(a.v[i], b.v[k - i], acc, hi);
+      mac_k(m[i], c::P_RAW[k - i], acc, hi);
+    }
+    t.v[k - 12] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t.v[11] = (uint32_t)acc;
+  return fp_reduce_once(t);
+}
+
+CESS_HD fp sqr(const fp& a) { return mul(a, a); }
+
+// a * 2^k-ish small multiples by repeated addition
+CESS_HD fp mul3(const fp& a) { return add(dbl(a), a); }
+CESS_HD fp mul4(const fp& a) { return dbl(dbl(a)); }
+CESS_HD fp mul8(const fp& a) { return dbl(dbl(dbl(a))); }
+
+// canonical integer <-> Montgomery
+CESS_HD fp from_mont(const fp& a) {
+  fp one_raw = fp_zero();
+  one_raw.v[0] = 1;
+  return mul(a, one_raw);
+}
+CESS_HD fp to_mont(const fp& a_raw) { return mul(a_raw, fp_from(c::R2)); }
+
+// a^e for a fixed 12-word exponent (square-and-multiply, MSB first).
+// The branch on the exponent bit is wave-uniform.
+CESS_HD fp pow_fixed(const fp& a, const uint32_t (&e)[12]) {
+  fp r = fp_one();
+  bool started = false;
+  for (int w = 11; w >= 0; w--) {
+    uint32_t word = e[w];
+    for (int b = 31; b >= 0; b--) {
+      if (started) r = sqr(r);
+      if ((word >> b) & 1u) {
+        r = started ? mul(r, a) : a;
+        started = true;
+      }
+    }
+  }
+  return r;
+}
+
+CESS_HD fp inv(const fp& a) { return pow_fixed(a, c::EXP_INV); }  // inv(0) = 0
+
+// returns true and a root if a is a square
+CESS_HD bool sqrt(fp& r, const fp& a) {
+  r = pow_fixed(a, c::EXP_SQRT);
+  return eq(sqr(r), a);
+}
+
+// canonical compare: raw (non-Montgomery) a > (p-1)/2
+CESS_HD bool raw_gt_half(const fp& a_raw) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t d = (uint64_t)c::P_HALF_RAW[i] - a_raw.v[i] - borrow;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow != 0;  // (p-1)/2 - a < 0
+}
+CESS_HD bool lex_largest(const fp& a) { return raw_gt_half(from_mont(a)); }
+
+// raw a < p ?
+CESS_HD bool raw_lt_p(const fp& a_raw) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t d = (uint64_t)a_raw.v[i] - c::P_RAW[i] - borrow;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow != 0;
+}
+
+// 48 big-endian bytes -> raw limbs
+CESS_HD fp raw_from_be48(const uint8_t* b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  return r;
+}
+CESS_HD void raw_to_be48(const fp& a, uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = a.v[i] >> 24;
+    q[1] = a.v[i] >> 16;
+    q[2] = a.v[i] >> 8;
+    q[3] = a.v[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fp2 = Fp[u]/(u^2 + 1)
+// ---------------------------------------------------------------------------
+CESS_HD fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+CESS_HD fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+CESS_HD fp2 add(const fp2& a, const fp2& b) { return {add(a.c0, b.c0), add(a.c1, b.c1)}; }
+CESS_HD fp2 sub(const fp2& a, const fp2& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1)}; }
+CESS_HD fp2 dbl(const fp2& a) { return {dbl(a.c0), dbl(a.c1)}; }
+CESS_HD fp2 neg(const fp2& a) { return {neg(a.c0), neg(a.c1)}; }
+CESS_HD fp2 conj(const fp2& a) { return {a.c0, neg(a.c1)}; }
+CESS_HD bool is_zero(const fp2& a) { return is_zero(a.c0) && is_zero(a.c1); }
+CESS_HD bool eq(const fp2& a, const fp2& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1); }
+CESS_HD fp2 select(bool c, const fp2& a, const fp2& b) { return {select(c, a.c0, b.c0), select(c, a.c1, b.c1)}; }
+CESS_HD fp2 mul3(const fp2& a) { return {mul3(a.c0), mul3(a.c1)}; }
+CESS_HD fp2 mul4(const fp2& a) { return {mul4(a.c0), mul4(a.c1)}; }
+CESS_HD fp2 mul8(const fp2& a) { return {mul8(a.c0), mul8(a.c1)}; }
+
+CESS_HD fp2 mul(const fp2& a, const fp2& b) {
+  fp t0 = mul(a.c0, b.c0);
+  fp t1 = mul(a.c1, b.c1);
+  fp t2 = mul(add(a.c0, a.c1), add(b.c0, b.c1));
+  return {sub(t0, t1), sub(sub(t2, t0), t1)};
+}
+CESS_HD fp2 sqr(const fp2& a) {
+  fp t0 = mul(add(a.c0, a.c1), sub(a.c0, a.c1));
+  fp t1 = mul(a.c0, a.c1);
+  return {t0, dbl(t1)};
+}
+CESS_HD fp2 mul_fp(const fp2& a, const fp& s) { return {mul(a.c0, s), mul(a.c1, s)}; }
+// * xi = (1 + u)
+CESS_HD fp2 mul_nr(const fp2& a) { return {sub(a.c0, a.c1), add(a.c0, a.c1)}; }
+CESS_HD fp2 inv(const fp2& a) {
+  fp t = inv(add(sqr(a.c0), sqr(a.c1)));
+  return {mul(a.c0, t), neg(mul(a.c1, t))};
+}
+CESS_HD bool lex_largest(const fp2& a) {
+  fp c1 = from_mont(a.c1);
+  if (!is_zero(c1)) return raw_gt_half(c1);
+  return raw_gt_half(from_mont(a.c0));
+}
+
+// Square root in Fp2 via the norm (p = 3 mod 4): returns false if a is not a square.
+// Any root is acceptable: callers normalise the sign (lexicographic rule).
+CESS_HD bool sqrt(fp2& r, const fp2& a) {
+  if (is_zero(a.c1)) {
+    // a real: sqrt(a0) if a0 is a QR, else sqrt(-a0) * u
+    fp s;
+    if (sqrt(s, a.c0)) {
+      r = {s, fp_zero()};
+      return true;
+    }
+    bool ok = sqrt(s, neg(a.c0));
+    r = {fp_zero(), s};
+    return ok;
+  }
+  fp n = add(sqr(a.c0), sqr(a.c1));
+  fp s;
+  if (!sqrt(s, n)) return false;
+  // exactly one of (a0 + s)/2, (a0 - s)/2 is a nonzero square (a1 != 0)
+  const fp half = fp_from(c::HALF);
+  fp al = mul(add(a.c0, s), half);
+  fp t = pow_fixed(al, c::EXP_SQRT_RATIO);  // al^((p-3)/4)
+  if (!eq(mul(sqr(t), al), fp_one())) {
+    al = mul(sub(a.c0, s), half);
+    t = pow_fixed(al, c::EXP_SQRT_RATIO);
+  }
+  // x0 = sqrt(al) = t * al ; 1/x0 = t ; x1 = a1 / (2 x0) = a1 * t * half
+  fp x0 = mul(t, al);
+  fp x1 = mul(mul(a.c1, t), half);
+  r = {x0, x1};
+  return eq(sqr(r), a);
+}
+
+// ---------------------------------------------------------------------------
+// Fp6 = Fp2[v]/(v^3 - xi)
+// ---------------------------------------------------------------------------
+CESS_HD fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
+CESS_HD fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+CESS_HD fp6 add(const fp6& a, const fp6& b) { return {add(a.c0, b.c0), add(a.c1, b.c1), add(a.c2, b.c2)}; }
+CESS_HD fp6 sub(const fp6& a, const fp6& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1), sub(a.c2, b.c2)}; }
+CESS_HD fp6 neg(const fp6& a) { return {neg(a.c0), neg(a.c1), neg(a.c2)}; }
+CESS_HD fp6 dbl(const fp6& a) { return {dbl(a.c0), dbl(a.c1), dbl(a.c2)}; }
+CESS_HD bool eq(const fp6& a, const fp6& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1) && eq(a.c2, b.c2); }
+// * v
+CESS_HD fp6 mul_v(const fp6& a) { return {mul_nr(a.c2), a.c0, a.c1}; }
+
+CESS_HD fp6 mul(const fp6& a, const fp6& b) {
+  fp2 t0 = mul(a.c0, b.c0);
+  fp2 t1 = mul(a.c1, b.c1);
+  fp2 t2 = mul(a.c2, b.c2);
+  fp2 c0 = add(mul_nr(sub(sub(mul(add(a.c1, a.c2), add(b.c1, b.c2)), t1), t2)), t0);
+  fp2 c1 = add(sub(sub(mul(add(a.c0, a.c1), add(b.c0, b.c1)), t0), t1), mul_nr(t2));
+  fp2 c2 = add(sub(sub(mul(add(a.c0, a.c2), add(b.c0, b.c2)), t0), t2), t1);
+  return {c0, c1, c2};
+}
+CESS_HD fp6 sqr(const fp6& a) {
+  // CH-SQR2
+  fp2 s0 = sqr(a.c0);
+  fp2 ab = mul(a.c0, a.c1);
+  fp2 s1 = dbl(ab);
+  fp2 s2 = sqr(add(sub(a.c0, a.c1), a.c2));
+  fp2 bc = mul(a.c1, a.c2);
+  fp2 s3 = dbl(bc);
+  fp2 s4 = sqr(a.c2);
+  fp2 c0 = add(mul_nr(s3), s0);
+  fp2 c1 = add(mul_nr(s4), s1);
+  fp2 c2 = sub(sub(add(add(s1, s2), s3), s0), s4);
+  return {c0, c1, c2};
+}
+// a * (b0 + b1 v)
+CESS_HD fp6 mul_by_01(const fp6& a, const fp2& b0, const fp2& b1) {
+  fp2 t0 = mul(a.c0, b0);
+  fp2 t1 = mul(a.c1, b1);
+  fp2 c0 = add(mul_nr(mul(a.c2, b1)), t0);
+  fp2 c1 = sub(sub(mul(add(a.c0, a.c1), add(b0, b1)), t0), t1);
+  fp2 c2 = add(mul(a.c2, b0), t1);
+  return {c0, c1, c2};
+}
+// a * (b1 v)
+CESS_HD fp6 mul_by_1(const fp6& a, const fp2& b1) {
+  return {mul_nr(mul(a.c2, b1)), mul(a.c0, b1), mul(a.c1, b1)};
+}
+CESS_HD fp6 inv(const fp6& a) {
+  fp2 c0 = sub(sqr(a.c0), mul_nr(mul(a.c1, a.c2)));
+  fp2 c1 = sub(mul_nr(sqr(a.c2)), mul(a.c0, a.c1));
+  fp2 c2 = sub(sqr(a.c1), mul(a.c0, a.c2));
+  fp2 t = add(mul(a.c0, c0), mul_nr(add(mul(a.c2, c1), mul(a.c1, c2))));
+  t = inv(t);
+  return {mul(c0, t), mul(c1, t), mul(c2, t)};
+}
+
+// ---------------------------------------------------------------------------
+// Fp12 = Fp6[w]/(w^2 - v)
+// ---------------------------------------------------------------------------
+CESS_HD fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+CESS_HD bool eq(const fp12& a, const fp12& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1); }
+CESS_HD bool is_one(const fp12& a) { return eq(a, fp12_one()); }
+CESS_HD fp12 conj(const fp12& a) { return {a.c0, neg(a.c1)}; }
+
+CESS_HD fp12 mul(const fp12& a, const fp12& b) {
+  fp6 t0 = mul(a.c0, b.c0);
+  fp6 t1 = mul(a.c1, b.c1);
+  fp6 c1 = sub(sub(mul(add(a.c0, a.c1), add(b.c0, b.c1)), t0), t1);
+  fp6 c0 = add(t0, mul_v(t1));
+  return {c0, c1};
+}
+CESS_HD fp12 sqr(const fp12& a) {
+  fp6 ab = mul(a.c0, a.c1);
+  fp6 c0 = sub(sub(mul(add(a.c0, a.c1), add(a.c0, mul_v(a.c1))), ab), mul_v(ab));
+  return {c0, dbl(ab)};
+}
+// f * (c0 + c1 v + c4 v w)   (bls12_381 Fp12::mul_by_014)
+CESS_HD fp12 mul_by_014(const fp12& f, const fp2& c0, const fp2& c1, const fp2& c4) {
+  fp6 aa = mul_by_01(f.c0, c0, c1);
+  fp6 bb = mul_by_1(f.c1, c4);
+  fp2 o = add(c1, c4);
+  fp6 t = mul_by_01(add(f.c1, f.c0), c0, o);
+  fp6 r1 = sub(sub(t, aa), bb);
+  fp6 r0 = add(mul_v(bb), aa);
+  return {r0, r1};
+}
+CESS_HD fp12 inv(const fp12& a) {
+  fp6 t = sub(mul(a.c0, a.c0), mul_v(mul(a.c1, a.c1)));
+  t = inv(t);
+  return {mul(a.c0, t), neg(mul(a.c1, t))};
+}
+
+// Frobenius^k (k = 1, 2, 3): coefficient of w^i is conj^k(a_i) * gamma_{k,i}
+// w-basis order: c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2  (i = 0..5)
+CESS_HD fp2 frob_coeff(int k, int i) {
+  return {fp_from(c::FROB[k - 1][i][0]), fp_from(c::FROB[k - 1][i][1])};
+}
+template <int K>
+CESS_HD fp12 frobenius(const fp12& a) {
+  auto f = [](const fp2& x, int i) -> fp2 {
+    fp2 y = (K & 1) ? conj(x) : x;
+    if (i == 0) return y;
+    return mul(y, frob_coeff(K, i));
+  };
+  fp12 r;
+  r.c0.c0 = f(a.c0.c0, 0);
+  r.c1.c0 = f(a.c1.c0, 1);
+  r.c0.c1 = f(a.c0.c1, 2);
+  r.c1.c1 = f(a.c1.c1, 3);
+  r.c0.c2 = f(a.c0.c2, 4);
+  r.c1.c2 = f(a.c1.c2, 5);
+  return r;
+}
+
+// Granger-Scott squaring in the cyclotomic subgroup (eprint 2009/565)
+CESS_HD void fp4_square(fp2& c0, fp2& c1, const fp2& a, const fp2& b) {
+  fp2 t0 = sqr(a);
+  fp2 t1 = sqr(b);
+  c0 = add(mul_nr(t1), t0);
+  c1 = sub(sub(sqr(add(a, b)), t0), t1);
+}
+CESS_HD fp12 cyclotomic_square(const fp12& f) {
+  fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
+  fp2 z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fp2 t0, t1, t2, t3;
+  fp4_square(t0, t1, z0, z1);
+  z0 = sub(t0, z0);
+  z0 = add(dbl(z0), t0);
+  z1 = add(t1, z1);
+  z1 = add(dbl(z1), t1);
+  fp4_square(t0, t1, z2, z3);
+  fp4_square(t2, t3, z4, z5);
+  z4 = sub(t0, z4);
+  z4 = add(dbl(z4), t0);
+  z5 = add(t1, z5);
+  z5 = add(dbl(z5), t1);
+  t0 = mul_nr(t3);
+  z2 = add(t0, z2);
+  z2 = add(dbl(z2), t0);
+  z3 = sub(t2, z3);
+  z3 = add(dbl(z3), t2);
+  fp12 r;
+  r.c0 = {z0, z4, z3};
+  r.c1 = {z2, z1, z5};
+  return r;
+}
+
+// f^x for x = -0xd201000000010000 in the cyclotomic subgroup
+CESS_HD fp12 cyclotomic_exp(const fp12& f) {
+  // |x| bits below the leading one (bit 63): 62, 60, 57, 48, 16
+  fp12 t = f;
+  for (int b = 62; b >= 0; b--) {
+    t = cyclotomic_square(t);
+    if (b == 62 || b == 60 || b == 57 || b == 48 || b == 16) t = mul(t, f);
+  }
+  return conj(t);
+}
+
+}  // namespace bls

@@ -1,0 +1,237 @@
+// RFC 9380 hash_to_curve BLS12381G1_XMD:SHA-256_SSWU_RO_ with the CESS DST.
+//
+// Replaces reference hash_to_g1 (utils/verify-bls-signatures/src/lib.rs:25-31):
+//   <G1Projective as HashToCurve<ExpandMsgXmd<Sha256>>>::hash_to_curve(msg, DST).to_affine()
+// Pipeline per message (one lane):
+//   expand_message_xmd (SHA-256; the 64-byte Z_pad block is a constant midstate;
+//   b1..b4 share a constant second block) -> u0, u1 = OS2IP(64 B) mod p
+//   -> simplified SWU on E' (RFC 9380 App. F.2 straight-line, sqrt_ratio for p = 3 mod 4)
+//   -> 11-isogeny evaluated homogeneously (no inversion) -> Q0 + Q1
+//   -> clear_cofactor [1 - x] -> one inversion to affine.
+#pragma once
+#include "curve.hpp"
+
+namespace bls {
+
+// ---------------------------------------------------------------------------
+// SHA-256 compression
+// ---------------------------------------------------------------------------
+CESS_CONST uint32_t SHA_K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+CESS_CONST uint32_t SHA_IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+CESS_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+CESS_HD void sha256_compress(uint32_t (&st)[8], const uint32_t (&blk)[16]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = blk[i];
+  uint32_t a = st[0], b = st[1], cc = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + ch + SHA_K[i] + wi;
+    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    uint32_t mj = (a & b) ^ (a & cc) ^ (b & cc);
+    uint32_t t2 = S0 + mj;
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = cc;
+    cc = b;
+    b = a;
+    a = t1 + t2;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += cc;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+// byte `pos` of the stream  msg || 0x00 0x80 || 0x00 || DST'  || SHA padding,
+// i.e. msg_prime of expand_message_xmd after the constant 64-byte Z_pad block.
+CESS_HD uint32_t xmd_b0_byte(const uint8_t* msg, uint32_t len, uint32_t pos, uint32_t padded) {
+  if (pos < len) return msg[pos];
+  uint32_t q = pos - len;
+  if (q == 0) return 0x00;   // I2OSP(128, 2)
+  if (q == 1) return 0x80;
+  if (q == 2) return 0x00;   // I2OSP(0, 1)
+  if (q < 3 + 44) return c::DST_PRIME[q - 3];
+  if (q == 47) return 0x80;  // SHA padding
+  if (pos >= padded - 8) {
+    uint64_t bits = (uint64_t)(64 + len + 47) * 8;
+    return (uint32_t)(bits >> (8 * (padded - 1 - pos))) & 0xff;
+  }
+  return 0;
+}
+
+// expand_message_xmd(msg, DST, 128) -> 32 big-endian words (b1 || b2 || b3 || b4)
+CESS_HD void expand_message_xmd_128(const uint8_t* msg, uint32_t len, uint32_t (&out)[32]) {
+  uint32_t b0[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) b0[i] = c::SHA_ZPAD_MID[i];
+  // bytes after the zero block: len + 47 data bytes + 1 + 8 padding, rounded to 64
+  uint32_t padded = ((len + 47 + 9) + 63) & ~63u;
+  for (uint32_t off = 0; off < padded; off += 64) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      uint32_t p0 = off + 4 * j;
+      blk[j] = (xmd_b0_byte(msg, len, p0, padded) << 24) | (xmd_b0_byte(msg, len, p0 + 1, padded) << 16) |
+               (xmd_b0_byte(msg, len, p0 + 2, padded) << 8) | xmd_b0_byte(msg, len, p0 + 3, padded);
+    }
+    sha256_compress(b0, blk);
+  }
+  // b_i = H((b0 ^ b_{i-1}) || i || DST'), 77 bytes = 2 blocks; block 2 is constant.
+  uint32_t blk2[16];
+  {
+    // DST'[31..44) (13 bytes) || 0x80 || 0... || bitlen 616
+    uint8_t t[64];
+#pragma unroll
+    for (int j = 0; j < 64; j++) t[j] = 0;
+#pragma unroll
+    for (int j = 0; j < 13; j++) t[j] = c::DST_PRIME[31 + j];
+    t[13] = 0x80;
+    t[62] = (616 >> 8) & 0xff;
+    t[63] = 616 & 0xff;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      blk2[j] = ((uint32_t)t[4 * j] << 24) | ((uint32_t)t[4 * j + 1] << 16) | ((uint32_t)t[4 * j + 2] << 8) | t[4 * j + 3];
+  }
+  uint32_t prev[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) prev[i] = 0;
+#pragma unroll
+  for (int idx = 1; idx <= 4; idx++) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int j = 0; j < 8; j++) blk[j] = b0[j] ^ prev[j];   // prev = 0 for b1
+    // byte 32 = idx, bytes 33..63 = DST'[0..31)
+    uint8_t t[32];
+    t[0] = (uint8_t)idx;
+#pragma unroll
+    for (int j = 0; j < 31; j++) t[1 + j] = c::DST_PRIME[j];
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      blk[8 + j] = ((uint32_t)t[4 * j] << 24) | ((uint32_t)t[4 * j + 1] << 16) | ((uint32_t)t[4 * j + 2] << 8) | t[4 * j + 3];
+    uint32_t st[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) st[j] = SHA_IV[j];
+    sha256_compress(st, blk);
+    sha256_compress(st, blk2);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      out[8 * (idx - 1) + j] = st[j];
+      prev[j] = st[j];
+    }
+  }
+}
+
+// 64 big-endian bytes (16 BE words) -> Montgomery(value mod p)
+CESS_HD fp fp_from_be64_words(const uint32_t* w) {
+  // value = H * 2^384 + L, H = words 0..3, L = words 4..15
+  fp lo, hi = fp_zero();
+#pragma unroll
+  for (int i = 0; i < 12; i++) lo.v[i] = w[15 - i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) hi.v[i] = w[3 - i];
+  return add(mul(lo, fp_from(c::R2)), mul(hi, fp_from(c::R3)));
+}
+
+CESS_HD uint32_t sgn0(const fp& a) { return from_mont(a).v[0] & 1u; }
+
+// simplified SWU onto E' : returns x = xn / xd and y (affine y)
+CESS_HD void map_to_curve_sswu(const fp& u, fp& xn, fp& xd, fp& y) {
+  const fp A = fp_from(c::ISO_A), B = fp_from(c::ISO_B), Z = fp_from(c::ISO_Z);
+  fp tv1 = mul(Z, sqr(u));             // Z u^2
+  fp tv2 = add(sqr(tv1), tv1);         // Z^2 u^4 + Z u^2
+  fp tv3 = mul(B, add(tv2, fp_one()));
+  fp tv4 = mul(A, select(is_zero(tv2), Z, neg(tv2)));
+  fp tv6 = sqr(tv4);
+  fp gxn = add(mul(add(sqr(tv3), mul(A, tv6)), tv3), mul(B, mul(tv6, tv4)));  // (tv3^2 + A tv6) tv3 + B tv6 tv4
+  fp gxd = mul(tv6, tv4);
+  // sqrt_ratio(gxn, gxd), q = 3 mod 4
+  fp s1 = sqr(gxd);
+  fp s2 = mul(gxn, gxd);
+  s1 = mul(s1, s2);
+  fp y1 = mul(pow_fixed(s1, c::EXP_SQRT_RATIO), s2);
+  fp y2 = mul(y1, fp_from(c::SSWU_C2));
+  bool is_qr = eq(mul(sqr(y1), gxd), gxn);
+  fp yy = select(is_qr, y1, y2);
+  fp x = mul(tv1, tv3);
+  fp ycand = mul(mul(tv1, u), yy);
+  xn = select(is_qr, tv3, x);
+  y = select(is_qr, yy, ycand);
+  if (sgn0(u) != sgn0(y)) y = neg(y);
+  xd = tv4;
+}
+
+// evaluate sum_i k_i xn^i xd^(deg-i) for a coefficient table of length n (deg = n-1)
+template <int N>
+CESS_HD fp iso_eval(const uint32_t (&k)[N][12], const fp (&xnp)[16], const fp (&xdp)[16], int deg) {
+  fp acc = fp_zero();
+#pragma unroll
+  for (int i = 0; i < N; i++) acc = add(acc, mul(fp_from(k[i]), mul(xnp[i], xdp[deg - i])));
+  return acc;
+}
+
+// 11-isogeny E' -> E, homogeneous output (X : Y : Z)
+CESS_HD g1p iso_map(const fp& xn, const fp& xd, const fp& y) {
+  fp xnp[16], xdp[16];
+  xnp[0] = fp_one();
+  xdp[0] = fp_one();
+#pragma unroll
+  for (int i = 1; i < 16; i++) {
+    xnp[i] = mul(xnp[i - 1], xn);
+    xdp[i] = mul(xdp[i - 1], xd);
+  }
+  // x = XN/XD with XN = xnum_h (deg 11), XD = xden_h (deg 10) * xd
+  fp XN = iso_eval(c::ISO_XNUM, xnp, xdp, 11);
+  fp XD = mul(iso_eval(c::ISO_XDEN, xnp, xdp, 10), xd);
+  // y = y * YN / YD, both degree 15
+  fp YN = iso_eval(c::ISO_YNUM, xnp, xdp, 15);
+  fp YD = iso_eval(c::ISO_YDEN, xnp, xdp, 15);
+  // (X : Y : Z) = (XN * YD : y * YN * XD : XD * YD)
+  return {mul(XN, YD), mul(mul(y, YN), XD), mul(XD, YD)};
+}
+
+CESS_HD g1a hash_to_g1(const uint8_t* msg, uint32_t len) {
+  uint32_t uni[32];
+  expand_message_xmd_128(msg, len, uni);
+  fp u0 = fp_from_be64_words(uni);
+  fp u1 = fp_from_be64_words(uni + 16);
+  fp xn, xd, y;
+  map_to_curve_sswu(u0, xn, xd, y);
+  g1p q0 = iso_map(xn, xd, y);
+  map_to_curve_sswu(u1, xn, xd, y);
+  g1p q1 = iso_map(xn, xd, y);
+  g1p r = proj_add(q0, q1);
+  r = proj_mul_u64(r, H_EFF_G1);
+  return proj_to_affine(r);
+}
+
+}  // namespace bls

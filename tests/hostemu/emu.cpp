@@ -1,0 +1,97 @@
+// TEST HARNESS ONLY: the device-side BLS headers compiled for the host
+// (CESS_HOSTEMU) so tests can check the kernel algorithms against the oracle on
+// a machine without a GPU.  Never linked into the product library.
+#include <string.h>
+#include "../../cess_amd/csrc/bls/h2c.hpp"
+#include "../../cess_amd/csrc/bls/pairing.hpp"
+
+using namespace bls;
+
+static void be_words(const uint8_t* b, int nwords, uint32_t* w) {
+  for (int i = 0; i < nwords; i++)
+    w[i] = ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) | ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];
+}
+static fp load_raw(const uint32_t* x) { fp r; memcpy(r.v, x, 48); return r; }
+static void store_raw(const fp& a, uint32_t* x) { fp r = from_mont(a); memcpy(x, r.v, 48); }
+
+extern "C" {
+void emu_fp_mul(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  store_raw(mul(to_mont(load_raw(a)), to_mont(load_raw(b))), out);
+}
+void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
+int emu_fp2_sqrt(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {
+  fp2 a = {to_mont(load_raw(a0)), to_mont(load_raw(a1))}, r;
+  bool ok = sqrt(r, a);
+  store_raw(r.c0, out0);
+  store_raw(r.c1, out1);
+  return ok;
+}
+// returns 1 valid, 0 invalid; out = x||y raw (identity: inf flag)
+int emu_decode_sig(const uint8_t* b, uint32_t* out, int* inf) {
+  uint32_t w[12];
+  be_words(b, 12, w);
+  g1a p;
+  bool ok = g1_decompress(w, p);
+  store_raw(p.x, out);
+  store_raw(p.y, out + 12);
+  *inf = p.inf;
+  return ok;
+}
+int emu_decode_pk(const uint8_t* b, uint32_t* out, int* inf) {
+  uint32_t w[24];
+  be_words(b, 24, w);
+  g2a p;
+  bool ok = g2_decompress(w, p);
+  store_raw(p.x.c0, out);
+  store_raw(p.x.c1, out + 12);
+  store_raw(p.y.c0, out + 24);
+  store_raw(p.y.c1, out + 36);
+  *inf = p.inf;
+  return ok;
+}
+void emu_hash(const uint8_t* msg, uint32_t len, uint32_t* out, int* inf) {
+  g1a h = hash_to_g1(msg, len);
+  store_raw(h.x, out);
+  store_raw(h.y, out + 12);
+  *inf = h.inf;
+}
+void emu_expand(const uint8_t* msg, uint32_t len, uint32_t* out32) {
+  uint32_t o[32];
+  expand_message_xmd_128(msg, len, o);
+  memcpy(out32, o, 128);
+}
+
+static coeff3 g_neg_g2[N_COEFFS];
+static bool g_init = false;
+static void init_neg_g2() {
+  if (g_init) return;
+  fp2 gx = {fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)};
+  fp2 gy = neg(fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)});
+  g2_prepare(gx, gy, [](int i, const coeff3& k) { g_neg_g2[i] = k; });
+  g_init = true;
+}
+
+// full per-signature verification with the kernel algorithms; gt_out (576 B) optional
+int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {
+  init_neg_g2();
+  uint32_t ws[12], wp[24];
+  be_words(sig, 12, ws);
+  be_words(pk, 24, wp);
+  g1a s;
+  if (!g1_decompress(ws, s)) return 2;
+  g2a q;
+  if (!g2_decompress(wp, q)) return 4;
+  g1a h = hash_to_g1(msg, mlen);
+  static coeff3 pkc[N_COEFFS];
+  fp2 qx = q.inf ? fp2{fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)} : q.x;
+  fp2 qy = q.inf ? fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)} : q.y;
+  g2_prepare(qx, qy, [](int i, const coeff3& k) { pkc[i] = k; });
+  fp12 f = miller_loop2(s, false, [](int i) { return g_neg_g2[i]; }, h, q.inf, [](int i) { return pkc[i]; });
+  fp12 g = final_exponentiation(f);
+  if (gt_out) {
+    const fp* e = &g.c0.c0.c0;
+    for (int i = 0; i < 12; i++) raw_to_be48(from_mont(e[i]), gt_out + 48 * i);
+  }
+  return is_one(g) ? 0 : 5;
+}
+}

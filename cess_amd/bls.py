@@ -1,0 +1,401 @@
+"""Host-side mirror of the reference crate `ic-verify-bls-signature`
+(/root/reference/utils/verify-bls-signatures/src/lib.rs) over the C ABI in
+include/cess_bls.h, plus the new batch entry point.
+
+Same names, argument meaning and error behaviour as the reference:
+  verify_bls_signature(sig, msg, key) -> Ok/Err            src/lib.rs:243-247
+  PublicKey.{BYTES, deserialize, serialize, verify}        src/lib.rs:33-101
+  Signature.{BYTES, deserialize, serialize}                src/lib.rs:113-153
+  PrivateKey.{BYTES, random, deserialize, serialize,
+              public_key, sign}                            src/lib.rs:166-237
+  InvalidPublicKey / InvalidSignature / InvalidPrivateKey  src/lib.rs:45-52, 104-110, 156-162
+New: verify_batch(records) -> Verdicts(bitmap, codes)      
+
+All arithmetic runs in the gfx950 kernels of libcess_bls.so.  There is no CPU
+fallback: without a HIP device every call raises DeviceUnavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+import secrets
+import threading
+from dataclasses import dataclass
+from typing import Iterable, Optional, Sequence, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CESS_BLS_LIB", os.path.join(_HERE, "lib", "libcess_bls.so"))
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+CODE_OK, CODE_SIG_LEN, CODE_SIG_POINT, CODE_PK_LEN, CODE_PK_POINT, CODE_PAIRING_FAIL = range(6)
+CODE_NAMES = {0: "OK", 1: "SIG_LEN", 2: "SIG_POINT", 3: "PK_LEN", 4: "PK_POINT", 5: "PAIRING_FAIL"}
+
+# the exported C symbols (tests check the library exports all of them)
+EXPORTS = (
+    "cess_bls_ctx_create", "cess_bls_ctx_destroy", "cess_bls_verify", "cess_bls_verify_batch",
+    "cess_bls_verify_batch_var", "cess_bls_verify_batch_device", "cess_bls_public_key_batch",
+    "cess_bls_sign_batch", "cess_bls_hash_to_g1_batch", "cess_bls_gt_batch", "cess_bls_stage_times",
+    "cess_bls_status_string", "cess_bls_version",
+)
+
+
+class DeviceUnavailable(RuntimeError):
+    """No usable HIP device / library: the verifier has no CPU fallback."""
+
+
+class BlsInfraError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("max_batch", ctypes.c_uint64), ("flags", ctypes.c_uint32)]
+
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libcess_bls.so and declare its C signatures (no device access)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise DeviceUnavailable(f"{path} not built (run __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        sz = ctypes.c_size_t
+        lib.cess_bls_ctx_create.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(vp)]
+        lib.cess_bls_ctx_destroy.argtypes = [vp]
+        lib.cess_bls_ctx_destroy.restype = None
+        lib.cess_bls_verify.argtypes = [vp, _u8p, sz, _u8p, sz, _u8p, sz, _u8p]
+        lib.cess_bls_verify_batch.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u64p]
+        lib.cess_bls_verify_batch_var.argtypes = [vp, sz, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p]
+        lib.cess_bls_verify_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
+        lib.cess_bls_public_key_batch.argtypes = [vp, sz, _u8p, _u8p]
+        lib.cess_bls_sign_batch.argtypes = [vp, sz, _u8p, _u8p, _u64p, _u8p]
+        lib.cess_bls_hash_to_g1_batch.argtypes = [vp, sz, _u8p, _u64p, _u8p]
+        lib.cess_bls_gt_batch.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p]
+        lib.cess_bls_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                             ctypes.c_int, ctypes.c_int]
+        lib.cess_bls_status_string.restype = ctypes.c_char_p
+        lib.cess_bls_status_string.argtypes = [ctypes.c_int]
+        lib.cess_bls_version.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def _buf(b: bytes):
+    if not b:
+        return ctypes.cast(ctypes.c_char_p(b"\0"), _u8p)
+    return ctypes.cast(ctypes.c_char_p(bytes(b)), _u8p)
+
+
+def _offsets(lengths: Sequence[int]):
+    arr = (ctypes.c_uint64 * (len(lengths) + 1))()
+    acc = 0
+    for i, n in enumerate(lengths):
+        arr[i] = acc
+        acc += n
+    arr[len(lengths)] = acc
+    return arr
+
+
+class Context:
+    """One GPU: device buffers, stream and the -G2 prepared table."""
+
+    def __init__(self, device: int = 0, max_batch: int = 1 << 20, profile: bool = False):
+        lib = load_library()
+        self._lib = lib
+        cfg = _Config(device, max_batch, 1 if profile else 0)
+        h = ctypes.c_void_p()
+        st = lib.cess_bls_ctx_create(ctypes.byref(cfg), ctypes.byref(h))
+        if st != 0:
+            msg = lib.cess_bls_status_string(st).decode()
+            if st == -2:
+                raise DeviceUnavailable(msg)
+            raise BlsInfraError(msg)
+        self._h = h
+        self.device = device
+        self.max_batch = max_batch
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.cess_bls_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st):
+        if st != 0:
+            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode())
+
+    @property
+    def handle(self):
+        return self._h
+
+    # --- verification ---------------------------------------------------
+    def verify_codes(self, records: Sequence[Tuple[bytes, bytes, bytes]]) -> bytes:
+        """Per-record verdict codes for (sig, msg, key) triples of any lengths."""
+        n = len(records)
+        if n == 0:
+            return b""
+        sigs = [bytes(r[0]) for r in records]
+        msgs = [bytes(r[1]) for r in records]
+        keys = [bytes(r[2]) for r in records]
+        codes = (ctypes.c_uint8 * n)()
+        bitmap = (ctypes.c_uint64 * ((n + 63) // 64))()
+        if all(len(s) == 48 for s in sigs) and all(len(k) == 96 for k in keys):
+            self._chk(self._lib.cess_bls_verify_batch(
+                self._h, n, _buf(b"".join(sigs)), _buf(b"".join(keys)), _buf(b"".join(msgs)),
+                _offsets([len(m) for m in msgs]), codes, bitmap))
+        else:
+            self._chk(self._lib.cess_bls_verify_batch_var(
+                self._h, n, _buf(b"".join(sigs)), _offsets([len(s) for s in sigs]),
+                _buf(b"".join(keys)), _offsets([len(k) for k in keys]),
+                _buf(b"".join(msgs)), _offsets([len(m) for m in msgs]), codes, bitmap))
+        return bytes(codes)
+
+    def verify_fixed(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets) -> Tuple[bytes, list]:
+        """Fixed-stride batch over packed host buffers; returns (codes, bitmap words)."""
+        n = len(sigs) // 48
+        assert len(sigs) == 48 * n and len(pks) == 96 * n
+        offs = (ctypes.c_uint64 * (n + 1))(*msg_offsets)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        self._chk(self._lib.cess_bls_verify_batch(self._h, n, _buf(sigs), _buf(pks), _buf(msgs), offs, codes, bitmap))
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64]
+
+    def gt(self, records) -> Tuple[bytes, list]:
+        n = len(records)
+        sigs, msgs, keys = (b"".join(bytes(r[j]) for r in records) for j in (0, 1, 2))
+        codes = (ctypes.c_uint8 * n)()
+        gt = (ctypes.c_uint8 * (576 * n))()
+        self._chk(self._lib.cess_bls_gt_batch(self._h, n, _buf(sigs), _buf(keys), _buf(msgs),
+                                              _offsets([len(r[1]) for r in records]), codes, gt))
+        raw = bytes(gt)
+        return bytes(codes), [raw[576 * i:576 * (i + 1)] for i in range(n)]
+
+    def verify_device(self, n, d_sigs, d_pks, d_msgs, d_offs, d_codes, d_bitmap, stream=0):
+        """Device-resident batch (HBM pointers as ints); enqueued on `stream`, not synchronised."""
+        self._chk(self._lib.cess_bls_verify_batch_device(self._h, n, d_sigs, d_pks, d_msgs, d_offs, d_codes,
+                                                         d_bitmap, stream or None))
+
+    # --- generator side -------------------------------------------------
+    def public_keys(self, sks: Sequence[bytes]) -> list:
+        n = len(sks)
+        out = (ctypes.c_uint8 * (96 * max(n, 1)))()
+        self._chk(self._lib.cess_bls_public_key_batch(self._h, n, _buf(b"".join(sks)), out))
+        raw = bytes(out)
+        return [raw[96 * i:96 * (i + 1)] for i in range(n)]
+
+    def sign(self, sks: Sequence[bytes], msgs: Sequence[bytes]) -> list:
+        n = len(sks)
+        out = (ctypes.c_uint8 * (48 * max(n, 1)))()
+        self._chk(self._lib.cess_bls_sign_batch(self._h, n, _buf(b"".join(sks)), _buf(b"".join(msgs)),
+                                                _offsets([len(m) for m in msgs]), out))
+        raw = bytes(out)
+        return [raw[48 * i:48 * (i + 1)] for i in range(n)]
+
+    def hash_to_g1(self, msgs: Sequence[bytes]) -> list:
+        n = len(msgs)
+        out = (ctypes.c_uint8 * (48 * max(n, 1)))()
+        self._chk(self._lib.cess_bls_hash_to_g1_batch(self._h, n, _buf(b"".join(msgs)),
+                                                      _offsets([len(m) for m in msgs]), out))
+        raw = bytes(out)
+        return [raw[48 * i:48 * (i + 1)] for i in range(n)]
+
+    def stage_times(self, reset=True) -> dict:
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_double * 16)()
+        k = self._lib.cess_bls_stage_times(self._h, names, ms, 16, 1 if reset else 0)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+
+_default: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default
+    if _default is None:
+        _default = Context()
+    return _default
+
+
+# ---------------------------------------------------------------------------
+# reference API mirror
+# ---------------------------------------------------------------------------
+class Result:
+    """Rust Result<(), ()> stand-in: truthy iff Ok."""
+
+    __slots__ = ("ok",)
+
+    def __init__(self, ok: bool):
+        self.ok = ok
+
+    def is_ok(self):
+        return self.ok
+
+    def is_err(self):
+        return not self.ok
+
+    def __bool__(self):
+        return self.ok
+
+    def __repr__(self):
+        return "Ok(())" if self.ok else "Err(())"
+
+
+class InvalidPublicKey(enum.Enum):
+    WrongLength = 0
+    InvalidPoint = 1
+
+
+class InvalidSignature(enum.Enum):
+    WrongLength = 0
+    InvalidPoint = 1
+
+
+class InvalidPrivateKey(enum.Enum):
+    WrongLength = 0
+    OutOfRange = 1
+
+
+class DeserializeError(ValueError):
+    def __init__(self, kind):
+        super().__init__(kind.name)
+        self.kind = kind
+
+
+# a fixed valid (sig, pk) pair lets the GPU classify one half of a record alone
+_ID_SIG = bytes([0xC0]) + bytes(47)
+_ID_PK = bytes([0xC0]) + bytes(95)
+
+
+class PublicKey:
+    BYTES = 96
+
+    def __init__(self, raw: bytes):
+        self._raw = bytes(raw)
+
+    @classmethod
+    def deserialize(cls, b: bytes) -> "PublicKey":
+        b = bytes(b)
+        if len(b) != cls.BYTES:
+            raise DeserializeError(InvalidPublicKey.WrongLength)
+        code = default_context().verify_codes([(_ID_SIG, b"", b)])[0]
+        if code == CODE_PK_POINT:
+            raise DeserializeError(InvalidPublicKey.InvalidPoint)
+        return cls(b)
+
+    def serialize(self) -> bytes:
+        return self._raw
+
+    def verify(self, message: bytes, signature: "Signature") -> Result:
+        code = default_context().verify_codes([(signature.serialize(), message, self._raw)])[0]
+        return Result(code == CODE_OK)
+
+    def __eq__(self, other):
+        return isinstance(other, PublicKey) and other._raw == self._raw
+
+    def __repr__(self):
+        return f"PublicKey({self._raw.hex()})"
+
+
+class Signature:
+    BYTES = 48
+
+    def __init__(self, raw: bytes):
+        self._raw = bytes(raw)
+
+    @classmethod
+    def deserialize(cls, b: bytes) -> "Signature":
+        b = bytes(b)
+        if len(b) != cls.BYTES:
+            raise DeserializeError(InvalidSignature.WrongLength)
+        code = default_context().verify_codes([(b, b"", _ID_PK)])[0]
+        if code == CODE_SIG_POINT:
+            raise DeserializeError(InvalidSignature.InvalidPoint)
+        return cls(b)
+
+    def serialize(self) -> bytes:
+        return self._raw
+
+    def __eq__(self, other):
+        return isinstance(other, Signature) and other._raw == self._raw
+
+    def __repr__(self):
+        return f"Signature({self._raw.hex()})"
+
+
+class PrivateKey:
+    BYTES = 32
+
+    def __init__(self, k: int):
+        self._k = k
+
+    @classmethod
+    def random(cls) -> "PrivateKey":
+        while True:   # rejection sampling, src/lib.rs:185-198
+            k = int.from_bytes(secrets.token_bytes(32), "big")
+            if k < R_ORDER:
+                return cls(k)
+
+    @classmethod
+    def deserialize(cls, b: bytes) -> "PrivateKey":
+        b = bytes(b)
+        if len(b) != cls.BYTES:
+            raise DeserializeError(InvalidPrivateKey.WrongLength)
+        k = int.from_bytes(b, "big")
+        if k >= R_ORDER:
+            raise DeserializeError(InvalidPrivateKey.OutOfRange)
+        return cls(k)
+
+    def serialize(self) -> bytes:
+        return self._k.to_bytes(32, "big")
+
+    def public_key(self) -> PublicKey:
+        return PublicKey(default_context().public_keys([self.serialize()])[0])
+
+    def sign(self, message: bytes) -> Signature:
+        return Signature(default_context().sign([self.serialize()], [bytes(message)])[0])
+
+    def __eq__(self, other):
+        return isinstance(other, PrivateKey) and other._k == self._k
+
+    def __repr__(self):
+        return "PrivateKey(REDACTED)"
+
+
+def verify_bls_signature(sig: bytes, msg: bytes, key: bytes) -> Result:
+    """verify_bls_signature (src/lib.rs:243-247)."""
+    return Result(default_context().verify_codes([(sig, msg, key)])[0] == CODE_OK)
+
+
+@dataclass
+class Verdicts:
+    bitmap: list      # u64 words, bit i%64 of word i//64 = record i verified
+    codes: bytes      # per-record code (0 OK, 1..5 see CODE_NAMES)
+
+    def ok(self, i: int) -> bool:
+        return bool((self.bitmap[i >> 6] >> (i & 63)) & 1)
+
+
+def verify_batch(records: Iterable[Tuple[bytes, bytes, bytes]], ctx: Optional[Context] = None) -> Verdicts:
+    """New batch entry point: records of (sig, msg, key) -> Verdicts."""
+    records = list(records)
+    codes = (ctx or default_context()).verify_codes(records)
+    words = [0] * ((len(records) + 63) // 64)
+    for i, c in enumerate(codes):
+        if c == CODE_OK:
+            words[i >> 6] |= 1 << (i & 63)
+    return Verdicts(words, codes)

@@ -165,6 +165,7 @@ template <class F>
 CESS_HD proj<F> proj_mul_u64(const proj<F>& p, uint64_t k) {
   proj<F> acc = proj_identity<F>();
   bool started = false;
+#pragma unroll 1
   for (int b = 63; b >= 0; b--) {
     if (started) acc = proj_dbl(acc);
     if ((k >> b) & 1u) {
@@ -178,6 +179,7 @@ template <class F>
 CESS_HD proj<F> proj_mul_u64_mixed(const F& px, const F& py, uint64_t k) {
   proj<F> acc = proj_identity<F>();
   bool started = false;
+#pragma unroll 1
   for (int b = 63; b >= 0; b--) {
     if (started) acc = proj_dbl(acc);
     if ((k >> b) & 1u) {
@@ -195,7 +197,9 @@ constexpr uint64_t H_EFF_G1 = 0xd201000000010001ull;    // 1 - x
 template <class F>
 CESS_HD proj<F> proj_mul_scalar_mixed(const F& px, const F& py, const uint32_t (&k)[8]) {
   proj<F> acc = proj_identity<F>();
+#pragma unroll 1
   for (int w = 7; w >= 0; w--) {
+#pragma unroll 1
     for (int b = 31; b >= 0; b--) {
       acc = proj_dbl(acc);
       if ((k[w] >> b) & 1u) acc = proj_add_mixed(acc, px, py);

@@ -96,6 +96,7 @@ CESS_HD void expand_message_xmd_128(const uint8_t* msg, uint32_t len, uint32_t (
   for (int i = 0; i < 8; i++) b0[i] = c::SHA_ZPAD_MID[i];
   // bytes after the zero block: len + 47 data bytes + 1 + 8 padding, rounded to 64
   uint32_t padded = ((len + 47 + 9) + 63) & ~63u;
+#pragma unroll 1
   for (uint32_t off = 0; off < padded; off += 64) {
     uint32_t blk[16];
 #pragma unroll
@@ -125,7 +126,7 @@ CESS_HD void expand_message_xmd_128(const uint8_t* msg, uint32_t len, uint32_t (
   uint32_t prev[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) prev[i] = 0;
-#pragma unroll
+#pragma unroll 1
   for (int idx = 1; idx <= 4; idx++) {
     uint32_t blk[16];
 #pragma unroll
@@ -159,7 +160,7 @@ CESS_HD fp fp_from_be64_words(const uint32_t* w) {
   for (int i = 0; i < 12; i++) lo.v[i] = w[15 - i];
 #pragma unroll
   for (int i = 0; i < 4; i++) hi.v[i] = w[3 - i];
-  return add(mul(lo, fp_from(c::R2)), mul(hi, fp_from(c::R3)));
+  return add(mul(lo, fp_from(c::R2)), mul(hi, fp_from(c::R2_384)));
 }
 
 CESS_HD uint32_t sgn0(const fp& a) { return from_mont(a).v[0] & 1u; }
@@ -219,19 +220,22 @@ CESS_HD g1p iso_map(const fp& xn, const fp& xd, const fp& y) {
   return {mul(XN, YD), mul(mul(y, YN), XD), mul(XD, YD)};
 }
 
-CESS_HD g1a hash_to_g1(const uint8_t* msg, uint32_t len) {
+// hash_to_g1 up to the cofactor clearing (projective), one SSWU+isogeny copy
+CESS_HD g1p hash_to_g1_proj(const uint8_t* msg, uint32_t len) {
   uint32_t uni[32];
   expand_message_xmd_128(msg, len, uni);
-  fp u0 = fp_from_be64_words(uni);
-  fp u1 = fp_from_be64_words(uni + 16);
-  fp xn, xd, y;
-  map_to_curve_sswu(u0, xn, xd, y);
-  g1p q0 = iso_map(xn, xd, y);
-  map_to_curve_sswu(u1, xn, xd, y);
-  g1p q1 = iso_map(xn, xd, y);
-  g1p r = proj_add(q0, q1);
-  r = proj_mul_u64(r, H_EFF_G1);
-  return proj_to_affine(r);
+  g1p q[2];
+#pragma unroll 1
+  for (int j = 0; j < 2; j++) {
+    fp u = fp_from_be64_words(j ? uni + 16 : uni);
+    fp xn, xd, y;
+    map_to_curve_sswu(u, xn, xd, y);
+    q[j] = iso_map(xn, xd, y);
+  }
+  g1p r = proj_add(q[0], q[1]);
+  return proj_mul_u64(r, H_EFF_G1);
 }
+
+CESS_HD g1a hash_to_g1(const uint8_t* msg, uint32_t len) { return proj_to_affine(hash_to_g1_proj(msg, len)); }
 
 }  // namespace bls

@@ -72,6 +72,7 @@ template <class Sink>
 CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink) {
   g2p r = {qx, qy, fp2_one()};
   int idx = 0;
+#pragma unroll 1
   for (int b = 61; b >= 0; b--) {
     sink(idx++, doubling_step(r));
     if (loop_bit(b)) sink(idx++, addition_step(r, qx, qy));
@@ -83,59 +84,107 @@ CESS_HD fp12 ell(const fp12& f, const coeff3& k, const fp& px, const fp& py) {
   return mul_by_014(f, k.c2, mul_fp(k.c1, px), mul_fp(k.c0, py));
 }
 
-// Two-pair Miller loop sharing one accumulator.  srcA(idx)/srcB(idx) return the
-// coefficient triples; a pair whose G1 or G2 point is the identity is skipped.
-template <class SrcA, class SrcB>
-CESS_HD fp12 miller_loop2(const g1a& pa, bool skip_a, SrcA&& srcA, const g1a& pb, bool skip_b, SrcB&& srcB) {
-  bool ua = !(skip_a || pa.inf), ub = !(skip_b || pb.inf);
-  fp12 f = fp12_one();
+// Coefficient step s (0..67) is followed by f <- f^2 unless it is a doubling
+// step whose addition step follows, or the last step.
+CESS_HD bool square_after_step(int s) {
+  // step order: for b = 61..0: D(b) [A(b) if loop_bit(b)]; final D
   int idx = 0;
+#pragma unroll 1
   for (int b = 61; b >= 0; b--) {
-    if (ua) f = ell(f, srcA(idx), pa.x, pa.y);
-    if (ub) f = ell(f, srcB(idx), pb.x, pb.y);
-    idx++;
-    if (loop_bit(b)) {
-      if (ua) f = ell(f, srcA(idx), pa.x, pa.y);
-      if (ub) f = ell(f, srcB(idx), pb.x, pb.y);
-      idx++;
-    }
-    f = sqr(f);
+    int last = idx + (loop_bit(b) ? 1 : 0);
+    if (s >= idx && s <= last) return s == last;
+    idx = last + 1;
   }
-  if (ua) f = ell(f, srcA(idx), pa.x, pa.y);
-  if (ub) f = ell(f, srcB(idx), pb.x, pb.y);
+  return false;
+}
+
+// Two-pair Miller loop sharing one accumulator.  src(pair, idx) returns the
+// coefficient triple of pair 0 (sig, -G2) or 1 (H(m), pk); a pair whose G1 or
+// G2 point is the identity is skipped.  The body holds a single copy of the
+// sparse line multiplication and of the Fp12 squaring (code size on CDNA4).
+template <class Src>
+CESS_HD fp12 miller_loop2(const g1a& pa, bool skip_a, const g1a& pb, bool skip_b, Src&& src) {
+  bool use[2] = {!(skip_a || pa.inf), !(skip_b || pb.inf)};
+  fp12 f = fp12_one();
+#pragma unroll 1
+  for (int s = 0; s < N_COEFFS; s++) {
+#pragma unroll 1
+    for (int pair = 0; pair < 2; pair++) {
+      if (!use[pair]) continue;
+      const fp& px = pair ? pb.x : pa.x;
+      const fp& py = pair ? pb.y : pa.y;
+      f = ell(f, src(pair, s), px, py);
+    }
+    if (square_after_step(s)) f = sqr(f);
+  }
   return conj(f);   // x < 0
 }
+
+// ---------------------------------------------------------------------------
+// Final exponentiation.  The coarse Fp12 operations are out-of-line helpers
+// with pointer arguments so each exists once in the code object (instruction
+// cache / compile time); operands then live in per-lane scratch, which costs
+// far less than the 18-54 Fp multiplies each helper performs.
+// ---------------------------------------------------------------------------
+CESS_NOINLINE void fe_mul(fp12* r, const fp12* a, const fp12* b) { *r = mul(*a, *b); }
+CESS_NOINLINE void fe_cycsq(fp12* r, const fp12* a) { *r = cyclotomic_square(*a); }
+CESS_NOINLINE void fe_frob(fp12* r, const fp12* a, int k) {
+  fp12 x = *a;
+  fp2* v[6] = {&x.c0.c0, &x.c1.c0, &x.c0.c1, &x.c1.c1, &x.c0.c2, &x.c1.c2};
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    fp2 y = (k & 1) ? conj(*v[i]) : *v[i];
+    if (i) y = mul(y, frob_coeff(k, i));
+    *v[i] = y;
+  }
+  *r = x;
+}
+// r = a^x (x = -|x|) in the cyclotomic subgroup
+CESS_NOINLINE void fe_cycexp(fp12* r, const fp12* a) {
+  fp12 t = *a;
+#pragma unroll 1
+  for (int b = 62; b >= 0; b--) {
+    t = cyclotomic_square(t);
+    if (b == 62 || b == 60 || b == 57 || b == 48 || b == 16) fe_mul(&t, &t, a);
+  }
+  *r = conj(t);
+}
+CESS_NOINLINE void fe_inv(fp12* r, const fp12* a) { *r = inv(*a); }
 
 // MillerLoopResult::final_exponentiation: easy part (p^6 - 1)(p^2 + 1), then the
 // hard part from five cyclotomic exponentiations by x.  Result = e^3 (canonical).
 CESS_HD fp12 final_exponentiation(const fp12& f) {
-  fp12 t0 = conj(f);   // f^(p^6)
-  fp12 t1 = inv(f);
-  fp12 t2 = mul(t0, t1);
+  fp12 t0, t1, t2, t3, t4, t5, t6, fin = f;
+  t0 = conj(fin);   // f^(p^6)
+  fe_inv(&t1, &fin);
+  fe_mul(&t2, &t0, &t1);
   t1 = t2;
-  t2 = frobenius<2>(t2);
-  t2 = mul(t2, t1);
-  t1 = conj(cyclotomic_square(t2));
-  fp12 t3 = cyclotomic_exp(t2);
-  fp12 t4 = cyclotomic_square(t3);
-  fp12 t5 = mul(t1, t3);
-  t1 = cyclotomic_exp(t5);
-  t0 = cyclotomic_exp(t1);
-  fp12 t6 = cyclotomic_exp(t0);
-  t6 = mul(t6, t4);
-  t4 = cyclotomic_exp(t6);
+  fe_frob(&t2, &t2, 2);
+  fe_mul(&t2, &t2, &t1);
+  fe_cycsq(&t1, &t2);
+  t1 = conj(t1);
+  fe_cycexp(&t3, &t2);
+  fe_cycsq(&t4, &t3);
+  fe_mul(&t5, &t1, &t3);
+  fe_cycexp(&t1, &t5);
+  fe_cycexp(&t0, &t1);
+  fe_cycexp(&t6, &t0);
+  fe_mul(&t6, &t6, &t4);
+  fe_cycexp(&t4, &t6);
   t5 = conj(t5);
-  t4 = mul(t4, mul(t5, t2));
+  fe_mul(&t5, &t5, &t2);
+  fe_mul(&t4, &t4, &t5);
   t5 = conj(t2);
-  t1 = mul(t1, t2);
-  t1 = frobenius<3>(t1);
-  t6 = mul(t6, t5);
-  t6 = frobenius<1>(t6);
-  t3 = mul(t3, t0);
-  t3 = frobenius<2>(t3);
-  t3 = mul(t3, t1);
-  t3 = mul(t3, t6);
-  return mul(t3, t4);
+  fe_mul(&t1, &t1, &t2);
+  fe_frob(&t1, &t1, 3);
+  fe_mul(&t6, &t6, &t5);
+  fe_frob(&t6, &t6, 1);
+  fe_mul(&t3, &t3, &t0);
+  fe_frob(&t3, &t3, 2);
+  fe_mul(&t3, &t3, &t1);
+  fe_mul(&t3, &t3, &t6);
+  fe_mul(&t3, &t3, &t4);
+  return t3;
 }
 
 }  // namespace bls

@@ -15,7 +15,7 @@ BLS_X = 0xd201000000010000
 X = -BLS_X
 R = X**4 - X**2 + 1
 P = (X - 1) ** 2 * R // 3 + X
-RM = 1 << 384
+RM = 1 << 392   # Montgomery radix: 14 x 28-bit compute limbs
 
 ISO_A = 0x144698a3b8e9433d693a02c96d4982b0ea985383ee66a8d8e8981aefd881ac98936f8da0e0f97f5cf428082d584c1d
 ISO_B = 0x12e2908d11688030018b12e8753eee3b2016c1f0f24f4070a0b9c14fcef35ef55a23215a316ceaa5d1cc48e98e172be0
@@ -196,20 +196,24 @@ def main():
     out = []
     w = out.append
     w("// GENERATED by cess_amd/csrc/gen_consts.py — do not edit.")
-    w("// BLS12-381 constants, 12 x u32 little-endian limbs; MONT = Montgomery form (R = 2^384).")
+    w("// BLS12-381 constants, 12 x u32 little-endian limbs; MONT = Montgomery form (R = 2^392).")
     w("#pragma once")
     w("#include <stdint.h>")
+    w("#ifndef CESS_CONST")
+    w("#define CESS_CONST static constexpr")
+    w("#endif")
     w("namespace bls { namespace c {")
 
     def arr(name, v, n=12):
         w(f"CESS_CONST uint32_t {name}[{n}] = {{" + ", ".join(f"0x{x:08x}u" for x in limbs(v, n)) + "};")
 
     arr("P_RAW", P)
-    pinv = (-pow(P, -1, 1 << 32)) % (1 << 32)
-    w(f"CESS_CONST uint32_t PINV = 0x{pinv:08x}u;")
     arr("ONE", mont(1))
     arr("R2", RM * RM % P)
-    arr("R3", RM * RM * RM % P)
+    arr("R2_384", (1 << 384) * RM * RM % P)   # mul(H, .) = H * 2^384 * R
+    p28 = [(P >> (28 * i)) & 0xFFFFFFF for i in range(14)]
+    w("CESS_CONST uint32_t P28[14] = {" + ", ".join(f"0x{x:07x}u" for x in p28) + "};")
+    w(f"CESS_CONST uint32_t PINV28 = 0x{(-pow(P, -1, 1 << 28)) % (1 << 28):07x}u;")
     arr("HALF", mont((P + 1) // 2))
     arr("P_HALF_RAW", (P - 1) // 2)
     # exponents (raw integers, little-endian words)

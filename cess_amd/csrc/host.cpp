@@ -1,0 +1,397 @@
+// Host runtime behind include/cess_bls.h: one context per GPU, a HIP stream,
+// device stage buffers sized for one launch chunk, and the constant
+// G2PREPARED_NEG_G table (reference src/lib.rs:19-21) built once on the device.
+//
+// There is no CPU compute path: every verdict is produced by the gfx950 kernels.
+// Without a usable HIP device, cess_bls_ctx_create fails with CESS_BLS_E_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/cess_bls.h"
+#include "bls/consts.hpp"
+#include "kernels.hpp"
+
+// kernels (k_*.hip)
+__global__ void k_decode_sig(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*, uint32_t*, uint64_t);
+__global__ void k_decode_pk(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*, uint32_t*, uint64_t);
+__global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*, uint32_t*, uint64_t);
+__global__ void k_prepare(uint64_t, const uint32_t*, uint32_t*, uint64_t);
+__global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                         const uint32_t*, uint32_t*, uint64_t);
+__global__ void k_final(uint64_t, uint8_t*, const uint32_t*, uint64_t*, uint8_t*, uint64_t);
+__global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
+__global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
+__global__ void k_hash_out(uint64_t, const uint8_t*, const uint64_t*, uint8_t*);
+
+namespace {
+
+enum Stage { ST_DECODE_SIG, ST_DECODE_PK, ST_HASH, ST_PREPARE, ST_MILLER, ST_FINAL, ST_N };
+const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk", "k_hash", "k_prepare", "k_miller", "k_final"};
+constexpr int kBlock = 256;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want) {
+    if (want <= bytes) return CESS_BLS_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, want) != hipSuccess) return CESS_BLS_E_OOM;
+    bytes = want;
+    return CESS_BLS_OK;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+struct cess_bls_ctx {
+  int device = 0;
+  uint64_t cap = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  // stage buffers (SoA, stride = cap)
+  DevBuf pre, code, inf, sig_aff, pk_aff, h_aff, coeffs, fval, bitmap, neg_g2;
+  // staging for the host-buffer APIs
+  DevBuf in_sigs, in_pks, in_msgs, in_offs, out_gt, in_sks, out_bytes;
+  std::vector<uint8_t> h_pre;
+  // profiling
+  hipEvent_t ev[ST_N + 1] = {};
+  double stage_ms[ST_N] = {};
+};
+
+#define HIPCHK(x)                          \
+  do {                                     \
+    if ((x) != hipSuccess) return CESS_BLS_E_HIP; \
+  } while (0)
+
+static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+
+extern "C" const char* cess_bls_version(void) { return "cess_amd-bls 0.1 (gfx950)"; }
+
+extern "C" const char* cess_bls_status_string(int s) {
+  switch (s) {
+    case CESS_BLS_OK: return "ok";
+    case CESS_BLS_E_INVALID_ARG: return "invalid argument";
+    case CESS_BLS_E_NO_DEVICE: return "no HIP device (the verifier has no CPU fallback)";
+    case CESS_BLS_E_HIP: return "HIP runtime error";
+    case CESS_BLS_E_OOM: return "device out of memory";
+    case CESS_BLS_E_RCCL: return "RCCL error";
+  }
+  return "unknown status";
+}
+
+static int alloc_stage(cess_bls_ctx* c) {
+  uint64_t n = c->cap;
+  int r = CESS_BLS_OK;
+  r |= c->pre.ensure(n);
+  r |= c->code.ensure(n);
+  r |= c->inf.ensure(n);
+  r |= c->sig_aff.ensure(n * CESS_W_G1 * 4);
+  r |= c->pk_aff.ensure(n * CESS_W_G2 * 4);
+  r |= c->h_aff.ensure(n * CESS_W_G1 * 4);
+  r |= c->coeffs.ensure(n * (uint64_t)CESS_W_COEFFS * 4);
+  r |= c->fval.ensure(n * CESS_W_FP12 * 4);
+  r |= c->bitmap.ensure((n / 64 + 1) * 8);
+  return r ? CESS_BLS_E_OOM : CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** out) {
+  if (!out) return CESS_BLS_E_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CESS_BLS_E_NO_DEVICE;
+  cess_bls_ctx* c = new cess_bls_ctx();
+  c->device = (cfg && cfg->device >= 0) ? cfg->device : 0;
+  if (c->device < 0 || c->device >= ndev) {
+    delete c;
+    return CESS_BLS_E_INVALID_ARG;
+  }
+  uint64_t cap = (cfg && cfg->max_batch) ? cfg->max_batch : (1ull << 20);
+  c->cap = (cap + 63) & ~63ull;
+  c->flags = cfg ? cfg->flags : 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return CESS_BLS_E_HIP;
+  }
+  int r = alloc_stage(c);
+  if (r == CESS_BLS_OK) r = c->neg_g2.ensure(CESS_W_COEFFS * 4);
+  if (r != CESS_BLS_OK) {
+    cess_bls_ctx_destroy(c);
+    return r;
+  }
+  for (int i = 0; i <= ST_N; i++)
+    if (hipEventCreate(&c->ev[i]) != hipSuccess) {
+      cess_bls_ctx_destroy(c);
+      return CESS_BLS_E_HIP;
+    }
+  // G2PREPARED_NEG_G: prepare -G2 on the device with the same kernel (n = 1, stride = 1)
+  uint32_t aff[48];
+  {
+    using namespace bls::c;
+    const uint32_t* src[4] = {G2_GEN_X0, G2_GEN_X1, G2_GEN_Y0, G2_GEN_Y1};
+    for (int j = 0; j < 4; j++) memcpy(aff + 12 * j, src[j], 48);
+    // negate y (Montgomery values are < p): y -> p - y, per Fp component
+    for (int j = 2; j < 4; j++) {
+      uint64_t borrow = 0;
+      for (int k = 0; k < 12; k++) {
+        uint64_t d = (uint64_t)P_RAW[k] - aff[12 * j + k] - borrow;
+        aff[12 * j + k] = (uint32_t)d;
+        borrow = (d >> 63) & 1;
+      }
+    }
+  }
+  DevBuf tmp;
+  if (tmp.ensure(sizeof(aff)) != CESS_BLS_OK || hipMemcpy(tmp.p, aff, sizeof(aff), hipMemcpyHostToDevice) != hipSuccess) {
+    cess_bls_ctx_destroy(c);
+    return CESS_BLS_E_HIP;
+  }
+  hipLaunchKernelGGL(k_prepare, dim3(1), dim3(64), 0, c->stream, (uint64_t)1, tmp.as<uint32_t>(), c->neg_g2.as<uint32_t>(),
+                     (uint64_t)1);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+    cess_bls_ctx_destroy(c);
+    return CESS_BLS_E_HIP;
+  }
+  *out = c;
+  return CESS_BLS_OK;
+}
+
+extern "C" void cess_bls_ctx_destroy(cess_bls_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int i = 0; i <= ST_N; i++)
+    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+// Enqueue the verification pipeline for one chunk of n <= cap records.
+// sigs/pks/msgs/offs/codes/bitmap/pre are device pointers; gt (optional).
+static int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* sigs, const uint8_t* pks,
+                     const uint8_t* msgs, const uint64_t* offs, const uint8_t* pre, uint8_t* codes, uint64_t* bitmap,
+                     uint8_t* gt) {
+  const uint64_t st = c->cap;
+  const bool prof = (c->flags & CESS_BLS_F_PROFILE) != 0;
+  const unsigned g = grid_for(n);
+  uint8_t* inf = c->inf.as<uint8_t>();
+  if (prof) HIPCHK(hipEventRecord(c->ev[0], s));
+  hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, n, sigs, pre, codes, inf, c->sig_aff.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[1], s));
+  hipLaunchKernelGGL(k_decode_pk, dim3(g), dim3(kBlock), 0, s, n, pks, pre, codes, inf, c->pk_aff.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[2], s));
+  hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes, c->h_aff.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[3], s));
+  hipLaunchKernelGGL(k_prepare, dim3(g), dim3(kBlock), 0, s, n, (const uint32_t*)c->pk_aff.as<uint32_t>(),
+                     c->coeffs.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[4], s));
+  hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
+                     (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint32_t*)c->coeffs.as<uint32_t>(),
+                     c->fval.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
+  hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, (const uint32_t*)c->fval.as<uint32_t>(), bitmap, gt, st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[6], s));
+  HIPCHK(hipGetLastError());
+  return CESS_BLS_OK;
+}
+
+static int collect_profile(cess_bls_ctx* c, hipStream_t s) {
+  if (!(c->flags & CESS_BLS_F_PROFILE)) return CESS_BLS_OK;
+  HIPCHK(hipStreamSynchronize(s));
+  for (int i = 0; i < ST_N; i++) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+    c->stage_ms[i] += ms;
+  }
+  return CESS_BLS_OK;
+}
+
+// Host-buffer batch over fixed-stride inputs (pre: optional host pre-flags)
+static int verify_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                       const uint64_t* offs, const uint8_t* pre, uint8_t* codes_out, uint64_t* bitmap_out,
+                       uint8_t* gt_out) {
+  if (n == 0) return CESS_BLS_OK;
+  if (!sigs || !pks || !offs || (!msgs && offs[n] != offs[0])) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  std::vector<uint64_t> rebased;
+  std::vector<uint64_t> words;
+  for (size_t off = 0; off < n; off += c->cap) {
+    uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    uint64_t mb0 = offs[off], mb1 = offs[off + m];
+    if (mb1 < mb0) return CESS_BLS_E_INVALID_ARG;
+    rebased.resize(m + 1);
+    for (uint64_t j = 0; j <= m; j++) {
+      if (j && offs[off + j] < offs[off + j - 1]) return CESS_BLS_E_INVALID_ARG;
+      rebased[j] = offs[off + j] - mb0;
+    }
+    int r = CESS_BLS_OK;
+    r |= c->in_sigs.ensure(m * 48);
+    r |= c->in_pks.ensure(m * 96);
+    r |= c->in_msgs.ensure(std::max<uint64_t>(mb1 - mb0, 1));
+    r |= c->in_offs.ensure((m + 1) * 8);
+    if (gt_out) r |= c->out_gt.ensure(m * 576);
+    if (r) return CESS_BLS_E_OOM;
+    HIPCHK(hipMemcpyAsync(c->in_sigs.p, sigs + 48 * off, m * 48, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_pks.p, pks + 96 * off, m * 96, hipMemcpyHostToDevice, s));
+    if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+    const uint8_t* dpre = nullptr;
+    if (pre) {
+      HIPCHK(hipMemcpyAsync(c->pre.p, pre + off, m, hipMemcpyHostToDevice, s));
+      dpre = c->pre.as<uint8_t>();
+    }
+    if (gt_out) HIPCHK(hipMemsetAsync(c->out_gt.p, 0, m * 576, s));
+    r = run_chunk(c, s, m, c->in_sigs.as<uint8_t>(), c->in_pks.as<uint8_t>(), c->in_msgs.as<uint8_t>(),
+                  c->in_offs.as<uint64_t>(), dpre, c->code.as<uint8_t>(), c->bitmap.as<uint64_t>(),
+                  gt_out ? c->out_gt.as<uint8_t>() : nullptr);
+    if (r) return r;
+    if (codes_out) HIPCHK(hipMemcpyAsync(codes_out + off, c->code.p, m, hipMemcpyDeviceToHost, s));
+    if (gt_out) HIPCHK(hipMemcpyAsync(gt_out + 576 * off, c->out_gt.p, m * 576, hipMemcpyDeviceToHost, s));
+    uint64_t nw = (m + 63) / 64;
+    words.resize(nw);
+    HIPCHK(hipMemcpyAsync(words.data(), c->bitmap.p, nw * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (bitmap_out) memcpy(bitmap_out + off / 64, words.data(), nw * 8);
+    r = collect_profile(c, s);
+    if (r) return r;
+  }
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_verify_batch(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                     const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* codes_out,
+                                     uint64_t* bitmap_out) {
+  if (!c) return CESS_BLS_E_INVALID_ARG;
+  return verify_host(c, n, sigs, pks, msgs, msg_offsets, nullptr, codes_out, bitmap_out, nullptr);
+}
+
+extern "C" int cess_bls_gt_batch(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                                 const uint64_t* msg_offsets, uint8_t* codes_out, uint8_t* gt_out) {
+  if (!c || !gt_out) return CESS_BLS_E_INVALID_ARG;
+  return verify_host(c, n, sigs, pks, msgs, msg_offsets, nullptr, codes_out, nullptr, gt_out);
+}
+
+extern "C" int cess_bls_verify_batch_var(cess_bls_ctx* c, size_t n, const uint8_t* sig_data, const uint64_t* sig_offsets,
+                                         const uint8_t* pk_data, const uint64_t* pk_offsets, const uint8_t* msgs,
+                                         const uint64_t* msg_offsets, uint8_t* codes_out, uint64_t* bitmap_out) {
+  if (!c || !sig_offsets || !pk_offsets || !msg_offsets) return CESS_BLS_E_INVALID_ARG;
+  if (n == 0) return CESS_BLS_OK;
+  std::vector<uint8_t> sigs(n * 48, 0), pks(n * 96, 0), pre(n, 0);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t sl = sig_offsets[i + 1] - sig_offsets[i], pl = pk_offsets[i + 1] - pk_offsets[i];
+    if (sig_offsets[i + 1] < sig_offsets[i] || pk_offsets[i + 1] < pk_offsets[i]) return CESS_BLS_E_INVALID_ARG;
+    if (sl == 48) memcpy(&sigs[48 * i], sig_data + sig_offsets[i], 48);
+    else pre[i] |= PRE_SIG_LEN_BAD;
+    if (pl == 96) memcpy(&pks[96 * i], pk_data + pk_offsets[i], 96);
+    else pre[i] |= PRE_PK_LEN_BAD;
+  }
+  return verify_host(c, n, sigs.data(), pks.data(), msgs, msg_offsets, pre.data(), codes_out, bitmap_out, nullptr);
+}
+
+extern "C" int cess_bls_verify(cess_bls_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* msg, size_t msg_len,
+                               const uint8_t* key, size_t key_len, uint8_t* code_out) {
+  if (!c || !code_out || (!sig && sig_len) || (!key && key_len) || (!msg && msg_len)) return CESS_BLS_E_INVALID_ARG;
+  uint64_t so[2] = {0, sig_len}, po[2] = {0, key_len}, mo[2] = {0, msg_len};
+  static const uint8_t zero = 0;
+  return cess_bls_verify_batch_var(c, 1, sig ? sig : &zero, so, key ? key : &zero, po, msg ? msg : &zero, mo, code_out,
+                                   nullptr);
+}
+
+extern "C" int cess_bls_verify_batch_device(cess_bls_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_pks,
+                                            const uint8_t* d_msgs, const uint64_t* d_offs, uint8_t* d_codes,
+                                            uint64_t* d_bitmap, void* stream) {
+  if (!c || !d_sigs || !d_pks || !d_offs || !d_codes) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  for (size_t off = 0; off < n; off += c->cap) {
+    uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    int r = run_chunk(c, s, m, d_sigs + 48 * off, d_pks + 96 * off, d_msgs, d_offs + off, nullptr, d_codes + off,
+                      d_bitmap ? d_bitmap + off / 64 : c->bitmap.as<uint64_t>(), nullptr);
+    if (r) return r;
+    if (c->flags & CESS_BLS_F_PROFILE) {
+      r = collect_profile(c, s);
+      if (r) return r;
+    }
+  }
+  return CESS_BLS_OK;
+}
+
+// generator-side batches -----------------------------------------------------
+static int gen_batch(cess_bls_ctx* c, int kind, size_t n, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs,
+                     uint8_t* out) {
+  if (!c || !out) return CESS_BLS_E_INVALID_ARG;
+  if (n == 0) return CESS_BLS_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const size_t ob = kind == 0 ? 96 : 48;
+  std::vector<uint64_t> rebased;
+  for (size_t off = 0; off < n; off += c->cap) {
+    uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    int r = c->out_bytes.ensure(m * ob);
+    if (kind != 2) r |= c->in_sks.ensure(m * 32);
+    if (r) return CESS_BLS_E_OOM;
+    if (kind != 2) HIPCHK(hipMemcpyAsync(c->in_sks.p, sks + 32 * off, m * 32, hipMemcpyHostToDevice, s));
+    if (kind != 0) {
+      uint64_t mb0 = offs[off], mb1 = offs[off + m];
+      rebased.resize(m + 1);
+      for (uint64_t j = 0; j <= m; j++) rebased[j] = offs[off + j] - mb0;
+      r = c->in_msgs.ensure(std::max<uint64_t>(mb1 - mb0, 1)) | c->in_offs.ensure((m + 1) * 8);
+      if (r) return CESS_BLS_E_OOM;
+      if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+    }
+    unsigned g = grid_for(m);
+    if (kind == 0)
+      hipLaunchKernelGGL(k_keygen, dim3(g), dim3(kBlock), 0, s, m, c->in_sks.as<uint8_t>(), c->out_bytes.as<uint8_t>());
+    else if (kind == 1)
+      hipLaunchKernelGGL(k_sign, dim3(g), dim3(kBlock), 0, s, m, c->in_sks.as<uint8_t>(), c->in_msgs.as<uint8_t>(),
+                         c->in_offs.as<uint64_t>(), c->out_bytes.as<uint8_t>());
+    else
+      hipLaunchKernelGGL(k_hash_out, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
+                         c->out_bytes.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out + ob * off, c->out_bytes.p, m * ob, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_public_key_batch(cess_bls_ctx* c, size_t n, const uint8_t* sks, uint8_t* pks_out) {
+  if (!sks && n) return CESS_BLS_E_INVALID_ARG;
+  return gen_batch(c, 0, n, sks, nullptr, nullptr, pks_out);
+}
+extern "C" int cess_bls_sign_batch(cess_bls_ctx* c, size_t n, const uint8_t* sks, const uint8_t* msgs,
+                                   const uint64_t* offs, uint8_t* sigs_out) {
+  if ((!sks || !offs) && n) return CESS_BLS_E_INVALID_ARG;
+  return gen_batch(c, 1, n, sks, msgs, offs, sigs_out);
+}
+extern "C" int cess_bls_hash_to_g1_batch(cess_bls_ctx* c, size_t n, const uint8_t* msgs, const uint64_t* offs,
+                                         uint8_t* out48) {
+  if (!offs && n) return CESS_BLS_E_INVALID_ARG;
+  return gen_batch(c, 2, n, nullptr, msgs, offs, out48);
+}
+
+extern "C" int cess_bls_stage_times(cess_bls_ctx* c, const char** names, double* ms, int max, int reset) {
+  if (!c) return CESS_BLS_E_INVALID_ARG;
+  int k = std::min(max, (int)ST_N);
+  for (int i = 0; i < k; i++) {
+    if (names) names[i] = kStageNames[i];
+    if (ms) ms[i] = c->stage_ms[i];
+  }
+  if (reset)
+    for (int i = 0; i < ST_N; i++) c->stage_ms[i] = 0;
+  return ST_N;
+}

@@ -1,0 +1,71 @@
+// CDNA4 (gfx950) kernels for batch BLS12-381 verification — one lane = one signature.
+// Stage outputs live in HBM in limb-major SoA layout (soa.hpp).
+// k_decode_sig: 48-B G1 encoding -> affine sig + code 1/2   (reference src/lib.rs:138-152, A3)
+// k_decode_pk : 96-B G2 encoding -> affine pk  + code 3/4   (reference src/lib.rs:68-82, A5)
+#include <hip/hip_runtime.h>
+#include "soa.hpp"
+
+using namespace bls;
+using namespace cess;
+
+__global__ __launch_bounds__(256) void k_decode_sig(uint64_t n, const uint8_t* __restrict__ sigs,
+                                                     const uint8_t* __restrict__ pre, uint8_t* __restrict__ code,
+                                                     uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff,
+                                                     uint64_t stride) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t pc = pre ? pre[i] : 0;
+  uint8_t c = 0, f = 0;
+  g1a p;
+  p.inf = true;
+  p.x = fp_zero();
+  p.y = fp_one();
+  if (pc & PRE_SIG_LEN_BAD) {
+    c = CODE_SIG_LEN;
+  } else {
+    uint32_t w[12];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(sigs + 48 * i);
+#pragma unroll
+    for (int k = 0; k < 12; k++) w[k] = bswap(src[k]);
+    if (!g1_decompress(w, p)) c = CODE_SIG_POINT;
+    else if (p.inf) f |= INF_SIG;
+  }
+  st_fp(sig_aff, stride, i, p.x);
+  st_fp(sig_aff + 12 * stride, stride, i, p.y);
+  code[i] = c;
+  inf[i] = f;
+}
+
+__global__ __launch_bounds__(256) void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
+                                                    const uint8_t* __restrict__ pre, uint8_t* __restrict__ code,
+                                                    uint8_t* __restrict__ inf, uint32_t* __restrict__ pk_aff,
+                                                    uint64_t stride) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t pc = pre ? pre[i] : 0;
+  uint8_t c = code[i];
+  uint8_t f = inf[i];
+  g2a q;
+  q.inf = true;
+  q.x = {fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)};
+  q.y = {fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)};
+  if (c == 0) {
+    if (pc & PRE_PK_LEN_BAD) {
+      c = CODE_PK_LEN;
+    } else {
+      uint32_t w[24];
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(pks + 96 * i);
+#pragma unroll
+      for (int k = 0; k < 24; k++) w[k] = bswap(src[k]);
+      g2a d;
+      if (!g2_decompress(w, d)) c = CODE_PK_POINT;
+      else if (d.inf) f |= INF_PK;
+      else q = d;
+    }
+  }
+  // identity / rejected keys keep the generator so k_prepare stays well-defined
+  st_fp2(pk_aff, stride, i, q.x);
+  st_fp2(pk_aff + 24 * stride, stride, i, q.y);
+  code[i] = c;
+  inf[i] = f;
+}

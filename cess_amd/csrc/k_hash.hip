@@ -1,0 +1,25 @@
+// CDNA4 (gfx950) kernels for batch BLS12-381 verification — one lane = one signature.
+// Stage outputs live in HBM in limb-major SoA layout (soa.hpp).
+// k_hash: msg -> H(m) affine, RFC 9380 SSWU (reference src/lib.rs:25-31, A8/A9)
+#include <hip/hip_runtime.h>
+#include "soa.hpp"
+
+using namespace bls;
+using namespace cess;
+
+__global__ __launch_bounds__(256) void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,
+                                               const uint64_t* __restrict__ offs, const uint8_t* __restrict__ code,
+                                               uint32_t* __restrict__ h_aff, uint64_t stride) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a h;
+  h.x = fp_zero();
+  h.y = fp_one();
+  if (code[i] == 0) {
+    uint64_t o = offs[i];
+    uint32_t len = (uint32_t)(offs[i + 1] - o);
+    h = hash_to_g1(msgs + o, len);
+  }
+  st_fp(h_aff, stride, i, h.x);
+  st_fp(h_aff + 12 * stride, stride, i, h.y);
+}

@@ -1,0 +1,38 @@
+// CDNA4 (gfx950) kernels for batch BLS12-381 verification — one lane = one signature.
+// Stage outputs live in HBM in limb-major SoA layout (soa.hpp).
+// k_prepare        : pk -> 68 line-coefficient triples (G2Prepared::from, src/lib.rs:88, A11)
+//                    (also builds the G2PREPARED_NEG_G table once per context, src/lib.rs:19-21, A10)
+// k_miller         : (sig,-G2),(H,pk) -> Miller-loop value (multi_miller_loop, src/lib.rs:90-93, A12)
+#include <hip/hip_runtime.h>
+#include "soa.hpp"
+
+using namespace bls;
+using namespace cess;
+
+__global__ __launch_bounds__(256) void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_aff,
+                                                  uint32_t* __restrict__ coeffs, uint64_t stride) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp2 qx = ld_fp2(pk_aff, stride, i);
+  fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
+  g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff(coeffs, stride, i, k, c); });
+}
+
+__global__ __launch_bounds__(256) void k_miller(uint64_t n, const uint8_t* __restrict__ code,
+                                                 const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
+                                                 const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
+                                                 const uint32_t* __restrict__ coeffs, uint32_t* __restrict__ fout,
+                                                 uint64_t stride) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (code[i] != 0) return;
+  uint8_t f = inf[i];
+  g1a s = {ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), (f & INF_SIG) != 0};
+  g1a h = {ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), false};
+  fp12 r = miller_loop2(s, false, h, (f & INF_PK) != 0, [&](int pair, int k) {
+    return pair ? ld_coeff(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k);
+  });
+  const fp* e = &r.c0.c0.c0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) st_fp(fout + 12 * j * stride, stride, i, e[j]);
+}

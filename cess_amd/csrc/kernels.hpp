@@ -1,0 +1,23 @@
+// Shared definitions between the HIP kernels and the host runtime.
+#pragma once
+#include <stdint.h>
+
+// verdict codes; precedence: signature, then key, then pairing
+enum : uint8_t {
+  CODE_OK = 0,
+  CODE_SIG_LEN = 1,
+  CODE_SIG_POINT = 2,
+  CODE_PK_LEN = 3,
+  CODE_PK_POINT = 4,
+  CODE_PAIRING = 5,
+};
+// host-side pre-validation flags (variable-length API)
+enum : uint8_t { PRE_SIG_LEN_BAD = 1, PRE_PK_LEN_BAD = 2 };
+// identity flags
+enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
+
+// words per signature of each SoA stage buffer
+#define CESS_W_G1 24u          // affine G1
+#define CESS_W_G2 48u          // affine G2
+#define CESS_W_COEFFS 4896u    // 68 x 3 Fp2
+#define CESS_W_FP12 144u

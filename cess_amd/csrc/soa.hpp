@@ -1,0 +1,56 @@
+// SoA (limb-major) device-buffer helpers: element e of signature i lives at
+// buf[e * stride + i], so consecutive lanes touch consecutive words.
+#pragma once
+#include "bls/h2c.hpp"
+#include "bls/pairing.hpp"
+#include "kernels.hpp"
+
+namespace cess {
+using namespace bls;
+
+
+// --- SoA helpers -----------------------------------------------------------
+CESS_HD fp ld_fp(const uint32_t* __restrict__ base, uint64_t stride, uint64_t i) {
+  fp r;
+#pragma unroll
+  for (int k = 0; k < 12; k++) r.v[k] = base[k * stride + i];
+  return r;
+}
+CESS_HD void st_fp(uint32_t* __restrict__ base, uint64_t stride, uint64_t i, const fp& a) {
+#pragma unroll
+  for (int k = 0; k < 12; k++) base[k * stride + i] = a.v[k];
+}
+CESS_HD fp2 ld_fp2(const uint32_t* base, uint64_t stride, uint64_t i) {
+  return {ld_fp(base, stride, i), ld_fp(base + 12 * stride, stride, i)};
+}
+CESS_HD void st_fp2(uint32_t* base, uint64_t stride, uint64_t i, const fp2& a) {
+  st_fp(base, stride, i, a.c0);
+  st_fp(base + 12 * stride, stride, i, a.c1);
+}
+CESS_HD uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// coefficient triple k of one signature: 6 Fp = 72 words, at word offset 72*k
+CESS_HD coeff3 ld_coeff(const uint32_t* base, uint64_t stride, uint64_t i, int k) {
+  const uint32_t* b = base + (uint64_t)(72 * k) * stride;
+  return {ld_fp2(b, stride, i), ld_fp2(b + 24 * stride, stride, i), ld_fp2(b + 48 * stride, stride, i)};
+}
+CESS_HD void st_coeff(uint32_t* base, uint64_t stride, uint64_t i, int k, const coeff3& c) {
+  uint32_t* b = base + (uint64_t)(72 * k) * stride;
+  st_fp2(b, stride, i, c.c0);
+  st_fp2(b + 24 * stride, stride, i, c.c1);
+  st_fp2(b + 48 * stride, stride, i, c.c2);
+}
+// wave-uniform coefficient table (the -G2 constant): stride 1, same address in every lane
+CESS_HD coeff3 ld_coeff_uniform(const uint32_t* tab, int k) {
+  const uint32_t* b = tab + 72 * k;
+  coeff3 r;
+  fp* e = &r.c0.c0;
+#pragma unroll
+  for (int j = 0; j < 6; j++)
+#pragma unroll
+    for (int l = 0; l < 12; l++) e[j].v[l] = b[12 * j + l];
+  return r;
+}
+
+
+}  // namespace cess

@@ -86,7 +86,7 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   fp2 qx = q.inf ? fp2{fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)} : q.x;
   fp2 qy = q.inf ? fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)} : q.y;
   g2_prepare(qx, qy, [](int i, const coeff3& k) { pkc[i] = k; });
-  fp12 f = miller_loop2(s, false, [](int i) { return g_neg_g2[i]; }, h, q.inf, [](int i) { return pkc[i]; });
+  fp12 f = miller_loop2(s, false, h, q.inf, [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
   fp12 g = final_exponentiation(f);
   if (gt_out) {
     const fp* e = &g.c0.c0.c0;

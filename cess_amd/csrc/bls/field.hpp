@@ -37,6 +37,16 @@
 
 namespace bls {
 
+#if defined(CESS_COUNT_OPS)
+// host test harness only: Fp multiply / square counters (algorithmic work)
+inline uint64_t g_mul_count = 0, g_sqr_count = 0;
+#define CESS_COUNT_MUL() (++g_mul_count)
+#define CESS_COUNT_SQR() (++g_sqr_count)
+#else
+#define CESS_COUNT_MUL() ((void)0)
+#define CESS_COUNT_SQR() ((void)0)
+#endif
+
 struct fp {
   uint32_t v[12];
 };
@@ -212,6 +222,7 @@ CESS_HD fp mont28(Col&& col) {
 
 // a * b * 2^-392 mod p
 CESS_HD fp mul(const fp& a, const fp& b) {
+  CESS_COUNT_MUL();
   uint32_t x[14], y[14];
   unpack28(a, x);
   unpack28(b, y);
@@ -224,6 +235,7 @@ CESS_HD fp mul(const fp& a, const fp& b) {
 
 // a^2 * 2^-392 mod p: off-diagonal products once against a doubled operand
 CESS_HD fp sqr(const fp& a) {
+  CESS_COUNT_SQR();
   uint32_t x[14], x2[14];
   unpack28(a, x);
 #pragma unroll

@@ -1,0 +1,50 @@
+"""Multi-GPU sharding of a verification batch (one process per GPU).
+
+Signatures are independent (reference src/lib.rs:243 is per signature), so a
+batch shards by index with no exchange during compute.  The only collective is
+the all-gather of the per-rank verdict-bitmap words (RCCL over xGMI on the
+node; gloo in CPU tests), which gives every rank the full batch bitmap — what a
+node-side caller of verify_batch needs.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+
+def shard_range(n: int, rank: int, world: int, align: int = 64) -> Tuple[int, int]:
+    """Contiguous [start, end) of rank's shard; boundaries are multiples of
+    `align` (a whole number of bitmap words per rank) except the batch end."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    words = (n + align - 1) // align
+    per = words // world
+    extra = words % world
+    w0 = rank * per + min(rank, extra)
+    w1 = w0 + per + (1 if rank < extra else 0)
+    return min(n, w0 * align), min(n, w1 * align)
+
+
+def gather_bitmap(local_words, n: int, world: int, group=None):
+    """All-gather per-rank bitmap words (int64 tensor on the rank's device) into
+    the full batch bitmap (ceil(n/64) words).  Shards from shard_range are
+    word-aligned, so concatenation in rank order is the global bitmap."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return local_words
+    sizes = []
+    for r in range(world):
+        a, b = shard_range(n, r, world)
+        sizes.append((b - a + 63) // 64)
+    mx = max(sizes)
+    buf = torch.zeros(mx, dtype=torch.int64, device=local_words.device)
+    buf[: local_words.numel()] = local_words
+    out = torch.empty(world * mx, dtype=torch.int64, device=local_words.device)
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+        out = torch.cat(parts)
+    else:
+        dist.all_gather_into_tensor(out, buf, group=group)
+    return torch.cat([out[r * mx: r * mx + sizes[r]] for r in range(world)])

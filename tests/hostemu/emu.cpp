@@ -71,6 +71,39 @@ static void init_neg_g2() {
   g_init = true;
 }
 
+#if defined(CESS_COUNT_OPS)
+// per-stage (mul, sqr) counts for one valid record: out[2*stage + {0,1}],
+// stages: decode_sig, decode_pk, hash, prepare, miller, final
+void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint64_t* out) {
+  init_neg_g2();
+  uint32_t ws[12], wp[24];
+  be_words(sig, 12, ws);
+  be_words(pk, 24, wp);
+  auto snap = [&](int st) {
+    out[2 * st] = g_mul_count;
+    out[2 * st + 1] = g_sqr_count;
+    g_mul_count = g_sqr_count = 0;
+  };
+  g_mul_count = g_sqr_count = 0;
+  g1a s;
+  g1_decompress(ws, s);
+  snap(0);
+  g2a q;
+  g2_decompress(wp, q);
+  snap(1);
+  g1a h = hash_to_g1(msg, mlen);
+  snap(2);
+  static coeff3 pkc[N_COEFFS];
+  g2_prepare(q.x, q.y, [](int i, const coeff3& k) { pkc[i] = k; });
+  snap(3);
+  fp12 f = miller_loop2(s, false, h, false, [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+  snap(4);
+  fp12 g = final_exponentiation(f);
+  (void)g;
+  snap(5);
+}
+#endif
+
 // full per-signature verification with the kernel algorithms; gt_out (576 B) optional
 int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {
   init_neg_g2();

@@ -8,7 +8,7 @@
 using namespace bls;
 using namespace cess;
 
-__global__ __launch_bounds__(256) void k_decode_sig(uint64_t n, const uint8_t* __restrict__ sigs,
+__global__ CESS_LB void k_decode_sig(uint64_t n, const uint8_t* __restrict__ sigs,
                                                      const uint8_t* __restrict__ pre, uint8_t* __restrict__ code,
                                                      uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff,
                                                      uint64_t stride) {
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void k_decode_sig(uint64_t n, const uint8_t* _
   inf[i] = f;
 }
 
-__global__ __launch_bounds__(256) void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
+__global__ CESS_LB void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
                                                     const uint8_t* __restrict__ pre, uint8_t* __restrict__ code,
                                                     uint8_t* __restrict__ inf, uint32_t* __restrict__ pk_aff,
                                                     uint64_t stride) {

@@ -7,7 +7,7 @@
 using namespace bls;
 using namespace cess;
 
-__global__ __launch_bounds__(256) void k_final(uint64_t n, uint8_t* __restrict__ code,
+__global__ CESS_LB void k_final(uint64_t n, uint8_t* __restrict__ code,
                                                 const uint32_t* __restrict__ fin, uint64_t* __restrict__ bitmap,
                                                 uint8_t* __restrict__ gt_out, uint64_t stride) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

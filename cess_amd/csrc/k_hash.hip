@@ -7,7 +7,7 @@
 using namespace bls;
 using namespace cess;
 
-__global__ __launch_bounds__(256) void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,
+__global__ CESS_LB void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,
                                                const uint64_t* __restrict__ offs, const uint8_t* __restrict__ code,
                                                uint32_t* __restrict__ h_aff, uint64_t stride) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -9,7 +9,7 @@
 using namespace bls;
 using namespace cess;
 
-__global__ __launch_bounds__(256) void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_aff,
+__global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_aff,
                                                   uint32_t* __restrict__ coeffs, uint64_t stride) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -18,7 +18,7 @@ __global__ __launch_bounds__(256) void k_prepare(uint64_t n, const uint32_t* __r
   g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff(coeffs, stride, i, k, c); });
 }
 
-__global__ __launch_bounds__(256) void k_miller(uint64_t n, const uint8_t* __restrict__ code,
+__global__ CESS_LB void k_miller(uint64_t n, const uint8_t* __restrict__ code,
                                                  const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
                                                  const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
                                                  const uint32_t* __restrict__ coeffs, uint32_t* __restrict__ fout,

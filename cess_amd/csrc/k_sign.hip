@@ -22,7 +22,7 @@ __device__ void store_bytes(uint8_t* dst, const uint8_t* src, int n) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_keygen(uint64_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
+__global__ CESS_LB void k_keygen(uint64_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_keygen(uint64_t n, const uint8_t* __res
   store_bytes(out + 96 * i, b, 96);
 }
 
-__global__ __launch_bounds__(256) void k_sign(uint64_t n, const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,
+__global__ CESS_LB void k_sign(uint64_t n, const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,
                                                const uint64_t* __restrict__ offs, uint8_t* __restrict__ out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void k_sign(uint64_t n, const uint8_t* __restr
   store_bytes(out + 48 * i, b, 48);
 }
 
-__global__ __launch_bounds__(256) void k_hash_out(uint64_t n, const uint8_t* __restrict__ msgs,
+__global__ CESS_LB void k_hash_out(uint64_t n, const uint8_t* __restrict__ msgs,
                                                    const uint64_t* __restrict__ offs, uint8_t* __restrict__ out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -2,6 +2,13 @@
 #pragma once
 #include <stdint.h>
 
+// Register budget of the stage kernels: 256-thread blocks, at least
+// CESS_MIN_WAVES waves per SIMD (512 / CESS_MIN_WAVES VGPR+AGPR per lane).
+#ifndef CESS_MIN_WAVES
+#define CESS_MIN_WAVES 1
+#endif
+#define CESS_LB __launch_bounds__(256, CESS_MIN_WAVES)
+
 // verdict codes; precedence: signature, then key, then pairing
 enum : uint8_t {
   CODE_OK = 0,

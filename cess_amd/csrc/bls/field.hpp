@@ -77,16 +77,42 @@ CESS_HD fp fp_zero() {
 }
 CESS_HD fp fp_one() { return fp_from(c::ONE); }
 
+// 32-bit add/sub with carry: __builtin_addc/__builtin_subc lower to
+// v_add_co_u32 / v_addc_co_u32 (v_sub_co / v_subb_co) chains on gfx950 -- one
+// instruction per limb.  (A 64-bit "(uint64_t)a - b - borrow" formulation
+// compiles to ~8 VALU per limb.)
+#if defined(CESS_HOSTEMU) && !defined(__clang__)
+CESS_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  uint64_t s = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+CESS_HD uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  uint64_t d = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+#else
+CESS_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  unsigned c;
+  uint32_t r = __builtin_addc(a, b, cin, &c);
+  *cout = c;
+  return r;
+}
+CESS_HD uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  unsigned c;
+  uint32_t r = __builtin_subc(a, b, bin, &c);
+  *bout = c;
+  return r;
+}
+#endif
+
 // r = t - p if t >= p  (t < 2p)
 CESS_HD fp fp_reduce_once(const fp& t) {
   fp s;
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t d = (uint64_t)t.v[i] - c::P_RAW[i] - borrow;
-    s.v[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 12; i++) s.v[i] = subc32(t.v[i], c::P_RAW[i], borrow, &borrow);
   fp r;
 #pragma unroll
   for (int i = 0; i < 12; i++) r.v[i] = borrow ? t.v[i] : s.v[i];
@@ -97,11 +123,7 @@ CESS_HD fp add(const fp& a, const fp& b) {
   fp t;
   uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t s = (uint64_t)a.v[i] + b.v[i] + carry;
-    t.v[i] = (uint32_t)s;
-    carry = (uint32_t)(s >> 32);
-  }
+  for (int i = 0; i < 12; i++) t.v[i] = addc32(a.v[i], b.v[i], carry, &carry);
   return fp_reduce_once(t);  // a + b < 2p < 2^382: no carry out of limb 11
 }
 
@@ -109,21 +131,13 @@ CESS_HD fp sub(const fp& a, const fp& b) {
   fp t;
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
-    t.v[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 12; i++) t.v[i] = subc32(a.v[i], b.v[i], borrow, &borrow);
   // if borrow: add p back
-  uint32_t mask = 0u - borrow;
+  const uint32_t mask = 0u - borrow;
   uint32_t carry = 0;
   fp r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t s = (uint64_t)t.v[i] + (c::P_RAW[i] & mask) + carry;
-    r.v[i] = (uint32_t)s;
-    carry = (uint32_t)(s >> 32);
-  }
+  for (int i = 0; i < 12; i++) r.v[i] = addc32(t.v[i], c::P_RAW[i] & mask, carry, &carry);
   return r;
 }
 
@@ -141,11 +155,7 @@ CESS_HD fp neg(const fp& a) {
   fp r;
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t d = (uint64_t)c::P_RAW[i] - a.v[i] - borrow;
-    r.v[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 12; i++) r.v[i] = subc32(c::P_RAW[i], a.v[i], borrow, &borrow);
   bool z = is_zero(a);
 #pragma unroll
   for (int i = 0; i < 12; i++) r.v[i] = z ? 0u : r.v[i];
@@ -165,6 +175,23 @@ CESS_HD fp select(bool c, const fp& a, const fp& b) {  // c ? a : b
   for (int i = 0; i < 12; i++) r.v[i] = c ? a.v[i] : b.v[i];
   return r;
 }
+
+// --- sequencing ---------------------------------------------------------------
+// seq(x): an empty volatile asm that "rewrites" x in VGPRs.  Volatile asms keep
+// their program order, so routing every multiply's operands and result through
+// one serialises the Fp multiplies: LLVM otherwise interleaves the independent
+// multiplies of an Fp2/Fp6 product for ILP and needs 512+ registers for an Fp6
+// multiply (measured), spilling to scratch.  Within one multiply the column
+// accumulation keeps enough independent work for a wave.
+#if defined(CESS_HOSTEMU)
+CESS_HD void seq(fp&) {}
+#else
+CESS_HD void seq(fp& a) {
+  asm volatile(""
+               : "+v"(a.v[0]), "+v"(a.v[1]), "+v"(a.v[2]), "+v"(a.v[3]), "+v"(a.v[4]), "+v"(a.v[5]),
+                 "+v"(a.v[6]), "+v"(a.v[7]), "+v"(a.v[8]), "+v"(a.v[9]), "+v"(a.v[10]), "+v"(a.v[11]));
+}
+#endif
 
 // --- 28-bit compute domain ---------------------------------------------------
 constexpr uint32_t M28 = 0x0fffffffu;
@@ -221,26 +248,33 @@ CESS_HD fp mont28(Col&& col) {
 }
 
 // a * b * 2^-392 mod p
-CESS_HD fp mul(const fp& a, const fp& b) {
+CESS_HD fp mul(const fp& a0, const fp& b0) {
   CESS_COUNT_MUL();
+  fp a = a0, b = b0;
+  seq(a);
+  seq(b);
   uint32_t x[14], y[14];
   unpack28(a, x);
   unpack28(b, y);
-  return mont28([&](int k, uint64_t& acc) {
+  fp r = mont28([&](int k, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++)
       if (k - i >= 0 && k - i < 14) acc += (uint64_t)x[i] * y[k - i];
   });
+  seq(r);
+  return r;
 }
 
 // a^2 * 2^-392 mod p: off-diagonal products once against a doubled operand
-CESS_HD fp sqr(const fp& a) {
+CESS_HD fp sqr(const fp& a0) {
   CESS_COUNT_SQR();
+  fp a = a0;
+  seq(a);
   uint32_t x[14], x2[14];
   unpack28(a, x);
 #pragma unroll
   for (int i = 0; i < 14; i++) x2[i] = x[i] << 1;
-  return mont28([&](int k, uint64_t& acc) {
+  fp r = mont28([&](int k, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++) {
       const int j = k - i;
@@ -248,6 +282,8 @@ CESS_HD fp sqr(const fp& a) {
     }
     if ((k & 1) == 0 && (k >> 1) < 14) acc += (uint64_t)x[k >> 1] * x[k >> 1];
   });
+  seq(r);
+  return r;
 }
 
 // a * 2^k-ish small multiples by repeated addition
@@ -295,10 +331,7 @@ CESS_HD bool sqrt(fp& r, const fp& a) {
 CESS_HD bool raw_gt_half(const fp& a_raw) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t d = (uint64_t)c::P_HALF_RAW[i] - a_raw.v[i] - borrow;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 12; i++) (void)subc32(c::P_HALF_RAW[i], a_raw.v[i], borrow, &borrow);
   return borrow != 0;  // (p-1)/2 - a < 0
 }
 CESS_HD bool lex_largest(const fp& a) { return raw_gt_half(from_mont(a)); }
@@ -307,10 +340,7 @@ CESS_HD bool lex_largest(const fp& a) { return raw_gt_half(from_mont(a)); }
 CESS_HD bool raw_lt_p(const fp& a_raw) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t d = (uint64_t)a_raw.v[i] - c::P_RAW[i] - borrow;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 12; i++) (void)subc32(a_raw.v[i], c::P_RAW[i], borrow, &borrow);
   return borrow != 0;
 }
 

@@ -1,0 +1,315 @@
+// Staged Fp12 arithmetic: the 576-byte Fp12 operands of the Miller loop and of
+// the final exponentiation live OUTSIDE the register file -- in an LDS column
+// (the hot accumulator) or in an HBM slot (cold temporaries of the final
+// exponentiation) -- and every operation streams its Fp2 pieces in, computes in
+// VGPRs, and writes the result back in place.
+//
+// Why (MI355X, one signature per lane): an Fp12 is 144 dwords; a value-based
+// Fp12 multiply keeps ~4 of them live, which overflows the 256 arch VGPRs + 256
+// AGPRs and spills to scratch (measured: 2.2 KB/lane in the Miller loop,
+// 8.9 KB/lane in the final exponentiation, 30-34 % of wave cycles waiting on
+// those spills).  With the accumulator in LDS (144 dwords x 256 lanes = 144 KiB
+// of the CU's 160 KiB) the register working set is one Fp12 operation's
+// temporaries only.
+//
+// Replaces bls12_381 0.7.1's Fp12 Miller loop / final exponentiation called at
+// utils/verify-bls-signatures/src/lib.rs:90-95.
+//
+// Store concept: `fp2 ld(int k) const` / `void st(int k, const fp2&)`, with
+// k = 3*i + j addressing coefficient c_i.c_j of (c0 + c1 w), c_i = (c_i.c0 +
+// c_i.c1 v + c_i.c2 v^2).  Word w of the 144-word image = limb (w % 12) of Fp
+// component ((w / 12) % 2) of fp2 (w / 24); rows of 4 words are uint4.
+#pragma once
+#include "pairing.hpp"
+
+#if defined(CESS_HOSTEMU)
+#define CESS_MEMBAR() ((void)0)
+#else
+// compiler-only barrier: LDS/HBM operands are re-read after it instead of being
+// kept live in registers across phases (register working set control)
+#define CESS_MEMBAR() asm volatile("" ::: "memory")
+#endif
+
+namespace bls {
+
+#if !defined(CESS_HOSTEMU)
+// One lane's Fp12 in an LDS image F[36][256] (uint4 rows; lane t owns column t,
+// so a wave reads 16 consecutive bytes per lane: conflict-free ds_read_b128).
+struct LdsF12 {
+  uint4 (*F)[256];
+  uint32_t t;
+  CESS_HD fp2 ld(int k) const {
+    fp2 r;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      uint4 x = F[6 * k + q][t];
+      fp& d = q < 3 ? r.c0 : r.c1;
+      const int o = 4 * (q % 3);
+      d.v[o] = x.x, d.v[o + 1] = x.y, d.v[o + 2] = x.z, d.v[o + 3] = x.w;
+    }
+    return r;
+  }
+  CESS_HD void st(int k, const fp2& a) const {
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const fp& s = q < 3 ? a.c0 : a.c1;
+      const int o = 4 * (q % 3);
+      F[6 * k + q][t] = make_uint4(s.v[o], s.v[o + 1], s.v[o + 2], s.v[o + 3]);
+    }
+  }
+};
+
+// One lane's Fp12 in an HBM slot: 36 uint4 rows of `stride` lanes (SoA,
+// coalesced 1 KiB per wave per row).
+struct GlobF12 {
+  uint4* base;
+  uint64_t stride;
+  uint32_t i;
+  CESS_HD fp2 ld(int k) const {
+    fp2 r;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      uint4 x = base[(uint64_t)(6 * k + q) * stride + i];
+      fp& d = q < 3 ? r.c0 : r.c1;
+      const int o = 4 * (q % 3);
+      d.v[o] = x.x, d.v[o + 1] = x.y, d.v[o + 2] = x.z, d.v[o + 3] = x.w;
+    }
+    return r;
+  }
+  CESS_HD void st(int k, const fp2& a) const {
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const fp& s = q < 3 ? a.c0 : a.c1;
+      const int o = 4 * (q % 3);
+      base[(uint64_t)(6 * k + q) * stride + i] = make_uint4(s.v[o], s.v[o + 1], s.v[o + 2], s.v[o + 3]);
+    }
+  }
+};
+#endif
+
+// Plain-memory store (host emulation; also the Gt output path)
+struct ArrF12 {
+  fp12* p;
+  CESS_HD fp2 ld(int k) const { return (&p->c0.c0)[k]; }
+  CESS_HD void st(int k, const fp2& a) const { (&p->c0.c0)[k] = a; }
+};
+
+template <class S>
+CESS_HD fp6 ld6(const S& s, int h) {
+  return {s.ld(3 * h), s.ld(3 * h + 1), s.ld(3 * h + 2)};
+}
+template <class S>
+CESS_HD void st6(const S& s, int h, const fp6& a) {
+  s.st(3 * h, a.c0);
+  s.st(3 * h + 1, a.c1);
+  s.st(3 * h + 2, a.c2);
+}
+template <class D, class S>
+CESS_HD void copy12(const D& d, const S& s) {
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) d.st(k, s.ld(k));
+}
+template <class S>
+CESS_HD void set_one12(const S& s) {
+  s.st(0, fp2_one());
+#pragma unroll 1
+  for (int k = 1; k < 6; k++) s.st(k, fp2_zero());
+}
+template <class S>
+CESS_HD void conj12(const S& s) {
+#pragma unroll 1
+  for (int k = 3; k < 6; k++) s.st(k, neg(s.ld(k)));
+}
+template <class S>
+CESS_HD bool is_one12(const S& s) {
+  bool r = eq(s.ld(0), fp2_one());
+#pragma unroll 1
+  for (int k = 1; k < 6; k++) r = r && is_zero(s.ld(k));
+  return r;
+}
+
+// f <- f^2  (complex squaring: 2 Fp6 multiplies)
+template <class S>
+CESS_HD void sqr12(const S& f) {
+  fp6 ab;
+  {
+    fp6 a0 = ld6(f, 0), a1 = ld6(f, 1);
+    ab = mul(a0, a1);
+  }
+  CESS_MEMBAR();
+  fp6 x;
+  {
+    fp6 a0 = ld6(f, 0), a1 = ld6(f, 1);
+    x = mul(add(a0, a1), add(a0, mul_v(a1)));
+  }
+  st6(f, 0, sub(sub(x, ab), mul_v(ab)));
+  st6(f, 1, dbl(ab));
+}
+
+// f <- f * (c0 + c1 v + c4 v w)   (bls12_381 Fp12::mul_by_014, in place)
+template <class S>
+CESS_HD void mul014(const S& f, const fp2& c0, const fp2& c1, const fp2& c4) {
+  fp6 bb = mul_by_1(ld6(f, 1), c4);
+  CESS_MEMBAR();
+  fp6 aa = mul_by_01(ld6(f, 0), c0, c1);
+  CESS_MEMBAR();
+  {
+    fp6 s = add(ld6(f, 0), ld6(f, 1));
+    st6(f, 1, s);                    // f.c1 <- a0 + a1 (consumed below)
+  }
+  st6(f, 0, add(mul_v(bb), aa));
+  fp6 u = add(aa, bb);
+  CESS_MEMBAR();
+  fp6 t = mul_by_01(ld6(f, 1), c0, add(c1, c4));
+  st6(f, 1, sub(t, u));
+}
+
+// f <- f * g  (Karatsuba over Fp6: 3 Fp6 multiplies)
+template <class S, class G>
+CESS_HD void mul12(const S& f, const G& g) {
+  fp6 t0, t1;
+  t0 = mul(ld6(f, 0), ld6(g, 0));
+  CESS_MEMBAR();
+  t1 = mul(ld6(f, 1), ld6(g, 1));
+  CESS_MEMBAR();
+  fp6 x = mul(add(ld6(f, 0), ld6(f, 1)), add(ld6(g, 0), ld6(g, 1)));
+  st6(f, 1, sub(sub(x, t0), t1));
+  st6(f, 0, add(t0, mul_v(t1)));
+}
+
+// f <- f^2 for f in the cyclotomic subgroup (Granger-Scott, eprint 2009/565)
+template <class S>
+CESS_HD void cycsq12(const S& f) {
+  // (z0,z1) = (c0.c0, c1.c1)
+  {
+    fp2 z0 = f.ld(0), z1 = f.ld(4), t0, t1;
+    fp4_square(t0, t1, z0, z1);
+    f.st(0, add(dbl(sub(t0, z0)), t0));
+    f.st(4, add(dbl(add(t1, z1)), t1));
+  }
+  CESS_MEMBAR();
+  // (z2,z3) = (c1.c0, c0.c2), (z4,z5) = (c0.c1, c1.c2)
+  fp2 t0, t1, t2, t3;
+  fp4_square(t0, t1, f.ld(3), f.ld(2));
+  fp4_square(t2, t3, f.ld(1), f.ld(5));
+  f.st(1, add(dbl(sub(t0, f.ld(1))), t0));
+  f.st(5, add(dbl(add(t1, f.ld(5))), t1));
+  fp2 n3 = mul_nr(t3);
+  f.st(3, add(dbl(add(n3, f.ld(3))), n3));
+  f.st(2, add(dbl(sub(t2, f.ld(2))), t2));
+}
+
+// f <- f^(p^k), k = 1, 2, 3.  w-basis index i of store index k': c0.c0=0,
+// c1.c0=1, c0.c1=2, c1.c1=3, c0.c2=4, c1.c2=5 (field.hpp frobenius).
+template <class S>
+CESS_HD void frob12(const S& f, int k) {
+#pragma unroll 1
+  for (int s = 0; s < 6; s++) {
+    const int i = (s % 3) * 2 + s / 3;
+    fp2 y = f.ld(s);
+    if (k & 1) y = conj(y);
+    if (i) y = mul(y, frob_coeff(k, i));
+    f.st(s, y);
+  }
+}
+
+// f <- f^-1
+template <class S>
+CESS_HD void inv12(const S& f) {
+  fp6 t;
+  {
+    fp6 a0 = ld6(f, 0), a1 = ld6(f, 1);
+    t = sub(sqr(a0), mul_v(sqr(a1)));
+  }
+  t = inv(t);
+  CESS_MEMBAR();
+  fp6 a0 = ld6(f, 0);
+  st6(f, 0, mul(a0, t));
+  fp6 a1 = ld6(f, 1);
+  st6(f, 1, neg(mul(a1, t)));
+}
+
+// ---------------------------------------------------------------------------
+// Final exponentiation as a program over one in-place accumulator A and HBM
+// slots (MillerLoopResult::final_exponentiation, A13).  Each opcode body exists
+// once in the code object; the hard part's five cyclotomic exponentiations by
+// x are spelled out as square runs and multiplies by the base.
+// ---------------------------------------------------------------------------
+enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_END };
+enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6, SL_N };
+
+// a^x (x = -0xd201000000010000) for a in slot s: bits below the top one are
+// 62, 60, 57, 48, 16 -> square runs 1, 2, 3, 9, 32, 16
+#define CESS_FE_CYCEXP(s) \
+  {FE_LOAD, s}, {FE_SQN, 1}, {FE_MUL, s}, {FE_SQN, 2}, {FE_MUL, s}, {FE_SQN, 3}, {FE_MUL, s}, {FE_SQN, 9}, \
+      {FE_MUL, s}, {FE_SQN, 32}, {FE_MUL, s}, {FE_SQN, 16}, {FE_CONJ, 0}
+
+// easy part: m = f^((p^6 - 1)(p^2 + 1)); hard part as in pairing.hpp
+// final_exponentiation (t2 = m).  SL_T0 doubles as scratch in the easy part.
+#define CESS_FE_PROGRAM                                                                                           \
+  {FE_LOAD, SL_F}, {FE_CONJ, 0}, {FE_STORE, SL_T0}, {FE_LOAD, SL_F}, {FE_INV, 0}, {FE_MUL, SL_T0},                 \
+      {FE_STORE, SL_T0}, {FE_FROB, 2}, {FE_MUL, SL_T0}, {FE_STORE, SL_M},                                          \
+      /* t1 = conj(cycsq(m)) */ {FE_SQN, 1}, {FE_CONJ, 0}, {FE_STORE, SL_T1},                                     \
+      /* t3 = m^x */ CESS_FE_CYCEXP(SL_M), {FE_STORE, SL_T3},                                                      \
+      /* t4 = cycsq(t3) */ {FE_SQN, 1}, {FE_STORE, SL_T4},                                                          \
+      /* t5 = t1 * t3 */ {FE_LOAD, SL_T1}, {FE_MUL, SL_T3}, {FE_STORE, SL_T5},                                     \
+      /* t1 = t5^x */ CESS_FE_CYCEXP(SL_T5), {FE_STORE, SL_T1},                                                    \
+      /* t0 = t1^x */ CESS_FE_CYCEXP(SL_T1), {FE_STORE, SL_T0},                                                    \
+      /* t6 = t0^x * t4 */ CESS_FE_CYCEXP(SL_T0), {FE_MUL, SL_T4}, {FE_STORE, SL_T6},                             \
+      /* t4 = t6^x */ CESS_FE_CYCEXP(SL_T6), {FE_STORE, SL_T4},                                                    \
+      /* t4 = t4 * conj(t5) * m */ {FE_LOAD, SL_T5}, {FE_CONJ, 0}, {FE_MUL, SL_M}, {FE_MUL, SL_T4},              \
+      {FE_STORE, SL_T4},                                                                                           \
+      /* t1 = frob3(t1 * m) */ {FE_LOAD, SL_T1}, {FE_MUL, SL_M}, {FE_FROB, 3}, {FE_STORE, SL_T1},                 \
+      /* t6 = frob1(t6 * conj(m)) */ {FE_LOAD, SL_M}, {FE_CONJ, 0}, {FE_MUL, SL_T6}, {FE_FROB, 1},              \
+      {FE_STORE, SL_T6},                                                                                           \
+      /* t3 = frob2(t3 * t0) * t1 * t6 * t4 */ {FE_LOAD, SL_T3}, {FE_MUL, SL_T0}, {FE_FROB, 2}, {FE_MUL, SL_T1},  \
+      {FE_MUL, SL_T6}, {FE_MUL, SL_T4}, {FE_END, 0}
+
+// Run the program.  `acc` is the accumulator store; slot(s) returns the store
+// of slot s (slot SL_F holds the Miller-loop output on entry).  Result in acc.
+template <class A, class SlotFn>
+CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& slot) {
+#pragma unroll 1
+  for (int pc = 0;; pc++) {
+    const uint8_t op = prog[pc][0], arg = prog[pc][1];
+    if (op == FE_END) break;
+    switch (op) {
+      case FE_LOAD: copy12(acc, slot(arg)); break;
+      case FE_STORE: copy12(slot(arg), acc); break;
+      case FE_MUL: mul12(acc, slot(arg)); break;
+      case FE_SQN:
+#pragma unroll 1
+        for (int r = 0; r < arg; r++) cycsq12(acc);
+        break;
+      case FE_CONJ: conj12(acc); break;
+      case FE_FROB: frob12(acc, arg); break;
+      case FE_INV: inv12(acc); break;
+      default: break;
+    }
+  }
+}
+
+// Miller loop for the two pairs of PublicKey::verify on an accumulator store:
+// pair 0 = (sig, -G2) (uniform -G2 table), pair 1 = (H(m), pk).
+template <class S, class Src>
+CESS_HD void miller_loop2_staged(const S& f, const g1a& pa, bool skip_a, const g1a& pb, bool skip_b, Src&& src) {
+  const bool use0 = !(skip_a || pa.inf), use1 = !(skip_b || pb.inf);
+  set_one12(f);
+#pragma unroll 1
+  for (int s = 0; s < N_COEFFS; s++) {
+#pragma unroll 1
+    for (int pair = 0; pair < 2; pair++) {
+      if (!(pair ? use1 : use0)) continue;
+      const fp& px = pair ? pb.x : pa.x;
+      const fp& py = pair ? pb.y : pa.y;
+      coeff3 k = src(pair, s);
+      mul014(f, k.c2, mul_fp(k.c1, px), mul_fp(k.c0, py));
+      CESS_MEMBAR();
+    }
+    if (square_after_step(s)) sqr12(f);
+    CESS_MEMBAR();
+  }
+  conj12(f);   // x < 0
+}
+
+}  // namespace bls

@@ -20,8 +20,8 @@ __global__ void k_decode_pk(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, 
 __global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*, uint32_t*, uint64_t);
 __global__ void k_prepare(uint64_t, const uint32_t*, uint32_t*, uint64_t);
 __global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                         const uint32_t*, uint32_t*, uint64_t);
-__global__ void k_final(uint64_t, uint8_t*, const uint32_t*, uint64_t*, uint8_t*, uint64_t);
+                         const uint32_t*, uint4*, uint64_t);
+__global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
 __global__ void k_hash_out(uint64_t, const uint8_t*, const uint64_t*, uint8_t*);
@@ -61,7 +61,7 @@ struct cess_bls_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   // stage buffers (SoA, stride = cap)
-  DevBuf pre, code, inf, sig_aff, pk_aff, h_aff, coeffs, fval, bitmap, neg_g2;
+  DevBuf pre, code, inf, sig_aff, pk_aff, h_aff, coeffs, fval, fe_slots, bitmap, neg_g2;
   // staging for the host-buffer APIs
   DevBuf in_sigs, in_pks, in_msgs, in_offs, out_gt, in_sks, out_bytes;
   std::vector<uint8_t> h_pre;
@@ -103,6 +103,7 @@ static int alloc_stage(cess_bls_ctx* c) {
   r |= c->h_aff.ensure(n * CESS_W_G1 * 4);
   r |= c->coeffs.ensure(n * (uint64_t)CESS_W_COEFFS * 4);
   r |= c->fval.ensure(n * CESS_W_FP12 * 4);
+  r |= c->fe_slots.ensure(n * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
   r |= c->bitmap.ensure((n / 64 + 1) * 8);
   return r ? CESS_BLS_E_OOM : CESS_BLS_OK;
 }
@@ -199,9 +200,10 @@ static int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* 
   hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
                      (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
                      (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint32_t*)c->coeffs.as<uint32_t>(),
-                     c->fval.as<uint32_t>(), st);
+                     c->fval.as<uint4>(), st);
   if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
-  hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, (const uint32_t*)c->fval.as<uint32_t>(), bitmap, gt, st);
+  hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,
+                     gt, st);
   if (prof) HIPCHK(hipEventRecord(c->ev[6], s));
   HIPCHK(hipGetLastError());
   return CESS_BLS_OK;

@@ -1,32 +1,41 @@
 // CDNA4 (gfx950) kernels for batch BLS12-381 verification — one lane = one signature.
-// Stage outputs live in HBM in limb-major SoA layout (soa.hpp).
 // k_final: final exponentiation -> code 0/5 + verdict bitmap (src/lib.rs:93-99, A13/A14)
+//
+// The exponentiation runs as a short program (bls/staged.hpp CESS_FE_PROGRAM)
+// over an accumulator held in LDS (144 KiB image for the block's 256 lanes) and
+// seven HBM slots (uint4 SoA, stride = context capacity) for the cold Fp12
+// temporaries; the Miller-loop output is slot SL_F.
 #include <hip/hip_runtime.h>
 #include "soa.hpp"
 
 using namespace bls;
 using namespace cess;
 
-__global__ CESS_LB void k_final(uint64_t n, uint8_t* __restrict__ code,
-                                                const uint32_t* __restrict__ fin, uint64_t* __restrict__ bitmap,
-                                                uint8_t* __restrict__ gt_out, uint64_t stride) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__constant__ uint8_t kFeProgram[][2] = {CESS_FE_PROGRAM};
+
+__global__ CESS_LB void k_final(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
+                                uint4* __restrict__ slots, uint64_t* __restrict__ bitmap,
+                                uint8_t* __restrict__ gt_out, uint64_t stride) {
+  __shared__ uint4 F[36][256];
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t c = CODE_SIG_LEN;
   if (i < n) {
     c = code[i];
     if (c == 0) {
-      fp12 f;
-      fp* e = &f.c0.c0.c0;
-#pragma unroll
-      for (int j = 0; j < 12; j++) e[j] = ld_fp(fin + 12 * j * stride, stride, i);
-      fp12 g = final_exponentiation(f);
-      if (!is_one(g)) c = CODE_PAIRING;
+      LdsF12 acc{F, threadIdx.x};
+      final_exp_staged(acc, kFeProgram, [&](int s) {
+        return GlobF12{s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride, stride, i};
+      });
+      if (!is_one12(acc)) c = CODE_PAIRING;
       if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
-        const fp* ge = &g.c0.c0.c0;
-        for (int j = 0; j < 12; j++) {
+#pragma unroll 1
+        for (int k = 0; k < 6; k++) {
+          fp2 e = acc.ld(k);
           uint8_t b[48];
-          raw_to_be48(from_mont(ge[j]), b);
-          for (int t = 0; t < 48; t++) gt_out[576 * i + 48 * j + t] = b[t];
+          raw_to_be48(from_mont(e.c0), b);
+          for (int t = 0; t < 48; t++) gt_out[576 * (uint64_t)i + 96 * k + t] = b[t];
+          raw_to_be48(from_mont(e.c1), b);
+          for (int t = 0; t < 48; t++) gt_out[576 * (uint64_t)i + 96 * k + 48 + t] = b[t];
         }
       }
       code[i] = c;

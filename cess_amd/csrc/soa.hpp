@@ -2,7 +2,7 @@
 // buf[e * stride + i], so consecutive lanes touch consecutive words.
 #pragma once
 #include "bls/h2c.hpp"
-#include "bls/pairing.hpp"
+#include "bls/staged.hpp"
 #include "kernels.hpp"
 
 namespace cess {
@@ -10,31 +10,31 @@ using namespace bls;
 
 
 // --- SoA helpers -----------------------------------------------------------
-CESS_HD fp ld_fp(const uint32_t* __restrict__ base, uint64_t stride, uint64_t i) {
+CESS_HD fp ld_fp(const uint32_t* __restrict__ base, uint64_t stride, uint32_t i) {
   fp r;
 #pragma unroll
   for (int k = 0; k < 12; k++) r.v[k] = base[k * stride + i];
   return r;
 }
-CESS_HD void st_fp(uint32_t* __restrict__ base, uint64_t stride, uint64_t i, const fp& a) {
+CESS_HD void st_fp(uint32_t* __restrict__ base, uint64_t stride, uint32_t i, const fp& a) {
 #pragma unroll
   for (int k = 0; k < 12; k++) base[k * stride + i] = a.v[k];
 }
-CESS_HD fp2 ld_fp2(const uint32_t* base, uint64_t stride, uint64_t i) {
+CESS_HD fp2 ld_fp2(const uint32_t* base, uint64_t stride, uint32_t i) {
   return {ld_fp(base, stride, i), ld_fp(base + 12 * stride, stride, i)};
 }
-CESS_HD void st_fp2(uint32_t* base, uint64_t stride, uint64_t i, const fp2& a) {
+CESS_HD void st_fp2(uint32_t* base, uint64_t stride, uint32_t i, const fp2& a) {
   st_fp(base, stride, i, a.c0);
   st_fp(base + 12 * stride, stride, i, a.c1);
 }
 CESS_HD uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
 // coefficient triple k of one signature: 6 Fp = 72 words, at word offset 72*k
-CESS_HD coeff3 ld_coeff(const uint32_t* base, uint64_t stride, uint64_t i, int k) {
+CESS_HD coeff3 ld_coeff(const uint32_t* base, uint64_t stride, uint32_t i, int k) {
   const uint32_t* b = base + (uint64_t)(72 * k) * stride;
   return {ld_fp2(b, stride, i), ld_fp2(b + 24 * stride, stride, i), ld_fp2(b + 48 * stride, stride, i)};
 }
-CESS_HD void st_coeff(uint32_t* base, uint64_t stride, uint64_t i, int k, const coeff3& c) {
+CESS_HD void st_coeff(uint32_t* base, uint64_t stride, uint32_t i, int k, const coeff3& c) {
   uint32_t* b = base + (uint64_t)(72 * k) * stride;
   st_fp2(b, stride, i, c.c0);
   st_fp2(b + 24 * stride, stride, i, c.c1);

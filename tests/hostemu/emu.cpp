@@ -3,7 +3,7 @@
 // a machine without a GPU.  Never linked into the product library.
 #include <string.h>
 #include "../../cess_amd/csrc/bls/h2c.hpp"
-#include "../../cess_amd/csrc/bls/pairing.hpp"
+#include "../../cess_amd/csrc/bls/staged.hpp"
 
 using namespace bls;
 
@@ -119,12 +119,42 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   fp2 qx = q.inf ? fp2{fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)} : q.x;
   fp2 qy = q.inf ? fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)} : q.y;
   g2_prepare(qx, qy, [](int i, const coeff3& k) { pkc[i] = k; });
-  fp12 f = miller_loop2(s, false, h, q.inf, [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
-  fp12 g = final_exponentiation(f);
+  // the staged (store-based) Miller loop and final-exponentiation program the
+  // kernels run, on plain-memory stores; the value-based versions in
+  // pairing.hpp are kept as an independent cross-check (emu_gt_valuebased)
+  static fp12 f, acc, slots[SL_N];
+  static const uint8_t prog[][2] = {CESS_FE_PROGRAM};
+  miller_loop2_staged(ArrF12{&slots[SL_F]}, s, false, h, q.inf,
+                      [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+  final_exp_staged(ArrF12{&acc}, prog, [](int sl) { return ArrF12{&slots[sl]}; });
+  fp12 g = acc;
+  (void)f;
   if (gt_out) {
     const fp* e = &g.c0.c0.c0;
     for (int i = 0; i < 12; i++) raw_to_be48(from_mont(e[i]), gt_out + 48 * i);
   }
+  return is_one(g) ? 0 : 5;
+}
+
+// value-based Miller loop + final exponentiation (pairing.hpp) for the same record
+int emu_gt_valuebased(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {
+  init_neg_g2();
+  uint32_t ws[12], wp[24];
+  be_words(sig, 12, ws);
+  be_words(pk, 24, wp);
+  g1a s;
+  if (!g1_decompress(ws, s)) return 2;
+  g2a q;
+  if (!g2_decompress(wp, q)) return 4;
+  g1a h = hash_to_g1(msg, mlen);
+  static coeff3 pkc[N_COEFFS];
+  fp2 qx = q.inf ? fp2{fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)} : q.x;
+  fp2 qy = q.inf ? fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)} : q.y;
+  g2_prepare(qx, qy, [](int i, const coeff3& k) { pkc[i] = k; });
+  fp12 f = miller_loop2(s, false, h, q.inf, [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+  fp12 g = final_exponentiation(f);
+  const fp* e = &g.c0.c0.c0;
+  for (int i = 0; i < 12; i++) raw_to_be48(from_mont(e[i]), gt_out + 48 * i);
   return is_one(g) ? 0 : 5;
 }
 }

@@ -290,20 +290,21 @@ CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& s
 }
 
 // Miller loop for the two pairs of PublicKey::verify on an accumulator store:
-// pair 0 = (sig, -G2) (uniform -G2 table), pair 1 = (H(m), pk).
-template <class S, class Src>
-CESS_HD void miller_loop2_staged(const S& f, const g1a& pa, bool skip_a, const g1a& pb, bool skip_b, Src&& src) {
-  const bool use0 = !(skip_a || pa.inf), use1 = !(skip_b || pb.inf);
+// pair 0 = (sig, -G2) (uniform -G2 table), pair 1 = (H(m), pk).  use0/use1:
+// the pair's points are both non-identity (identity terms contribute 1).
+// pt(pair) yields the pair's affine G1 point; src(pair, step) its coefficients.
+template <class S, class Pt, class Src>
+CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src) {
   set_one12(f);
 #pragma unroll 1
   for (int s = 0; s < N_COEFFS; s++) {
 #pragma unroll 1
     for (int pair = 0; pair < 2; pair++) {
       if (!(pair ? use1 : use0)) continue;
-      const fp& px = pair ? pb.x : pa.x;
-      const fp& py = pair ? pb.y : pa.y;
       coeff3 k = src(pair, s);
-      mul014(f, k.c2, mul_fp(k.c1, px), mul_fp(k.c0, py));
+      g1a p = pt(pair);
+      fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
+      mul014(f, k.c2, c1, c4);
       CESS_MEMBAR();
     }
     if (square_after_step(s)) sqr12(f);

@@ -18,9 +18,9 @@
 __global__ void k_decode_sig(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*, uint32_t*, uint64_t);
 __global__ void k_decode_pk(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*, uint32_t*, uint64_t);
 __global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*, uint32_t*, uint64_t);
-__global__ void k_prepare(uint64_t, const uint32_t*, uint32_t*, uint64_t);
+__global__ void k_prepare(uint64_t, const uint32_t*, uint4*, uint64_t);
 __global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                         const uint32_t*, uint4*, uint64_t);
+                         const uint4*, uint4*, uint64_t);
 __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
@@ -158,7 +158,7 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
     cess_bls_ctx_destroy(c);
     return CESS_BLS_E_HIP;
   }
-  hipLaunchKernelGGL(k_prepare, dim3(1), dim3(64), 0, c->stream, (uint64_t)1, tmp.as<uint32_t>(), c->neg_g2.as<uint32_t>(),
+  hipLaunchKernelGGL(k_prepare, dim3(1), dim3(64), 0, c->stream, (uint64_t)1, tmp.as<uint32_t>(), c->neg_g2.as<uint4>(),
                      (uint64_t)1);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     cess_bls_ctx_destroy(c);
@@ -195,11 +195,11 @@ static int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* 
   hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes, c->h_aff.as<uint32_t>(), st);
   if (prof) HIPCHK(hipEventRecord(c->ev[3], s));
   hipLaunchKernelGGL(k_prepare, dim3(g), dim3(kBlock), 0, s, n, (const uint32_t*)c->pk_aff.as<uint32_t>(),
-                     c->coeffs.as<uint32_t>(), st);
+                     c->coeffs.as<uint4>(), st);
   if (prof) HIPCHK(hipEventRecord(c->ev[4], s));
   hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
                      (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
-                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint32_t*)c->coeffs.as<uint32_t>(),
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)c->coeffs.as<uint4>(),
                      c->fval.as<uint4>(), st);
   if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
   hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,

@@ -10,30 +10,34 @@ using namespace bls;
 using namespace cess;
 
 __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_aff,
-                                                  uint32_t* __restrict__ coeffs, uint64_t stride) {
+                                  uint4* __restrict__ coeffs, uint64_t stride) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   fp2 qx = ld_fp2(pk_aff, stride, i);
   fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
-  g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff(coeffs, stride, i, k, c); });
+  g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); });
 }
 
 // LDS image of the 256 lanes' Miller accumulators: 144 dwords x 256 = 144 KiB
 __global__ CESS_LB void k_miller(uint64_t n, const uint8_t* __restrict__ code,
                                  const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
                                  const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
-                                 const uint32_t* __restrict__ coeffs, uint4* __restrict__ fout,
+                                 const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
                                  uint64_t stride) {
   __shared__ uint4 F[36][256];
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (code[i] != 0) return;
   uint8_t fl = inf[i];
-  g1a s = {ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), (fl & INF_SIG) != 0};
-  g1a h = {ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), false};
   LdsF12 f{F, threadIdx.x};
-  miller_loop2_staged(f, s, false, h, (fl & INF_PK) != 0, [&](int pair, int k) {
-    return pair ? ld_coeff(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k);
-  });
+  // the G1 points are re-read from HBM (L2) for every line instead of being
+  // held in 48 registers across the loop
+  miller_loop2_staged(
+      f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0,
+      [&](int pair) {
+        const uint32_t* b = pair ? h_aff : sig_aff;
+        return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
+      },
+      [&](int pair, int k) { return pair ? ld_coeff4(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k); });
   copy12(GlobF12{fout, stride, i}, f);
 }

@@ -40,6 +40,23 @@ CESS_HD void st_coeff(uint32_t* base, uint64_t stride, uint32_t i, int k, const 
   st_fp2(b + 24 * stride, stride, i, c.c1);
   st_fp2(b + 48 * stride, stride, i, c.c2);
 }
+// uint4-row layout (k_prepare output): row q of step k of sig i at base[(18k+q)*stride + i]
+CESS_HD coeff3 ld_coeff4(const uint4* __restrict__ base, uint64_t stride, uint32_t i, int k) {
+  coeff3 r;
+  uint32_t* w = &r.c0.c0.v[0];
+#pragma unroll
+  for (int q = 0; q < 18; q++) {
+    uint4 x = base[(uint64_t)(18 * k + q) * stride + i];
+    w[4 * q] = x.x, w[4 * q + 1] = x.y, w[4 * q + 2] = x.z, w[4 * q + 3] = x.w;
+  }
+  return r;
+}
+CESS_HD void st_coeff4(uint4* __restrict__ base, uint64_t stride, uint32_t i, int k, const coeff3& c) {
+  const uint32_t* w = &c.c0.c0.v[0];
+#pragma unroll
+  for (int q = 0; q < 18; q++)
+    base[(uint64_t)(18 * k + q) * stride + i] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
 // wave-uniform coefficient table (the -G2 constant): stride 1, same address in every lane
 CESS_HD coeff3 ld_coeff_uniform(const uint32_t* tab, int k) {
   const uint32_t* b = tab + 72 * k;

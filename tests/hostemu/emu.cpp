@@ -124,7 +124,10 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   // pairing.hpp are kept as an independent cross-check (emu_gt_valuebased)
   static fp12 f, acc, slots[SL_N];
   static const uint8_t prog[][2] = {CESS_FE_PROGRAM};
-  miller_loop2_staged(ArrF12{&slots[SL_F]}, s, false, h, q.inf,
+  static g1a pts[2];
+  pts[0] = s;
+  pts[1] = h;
+  miller_loop2_staged(ArrF12{&slots[SL_F]}, !s.inf, !(q.inf || h.inf), [](int pair) { return pts[pair]; },
                       [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
   final_exp_staged(ArrF12{&acc}, prog, [](int sl) { return ArrF12{&slots[sl]}; });
   fp12 g = acc;

@@ -38,6 +38,7 @@ EXPORTS = (
     "cess_bls_verify_batch_var", "cess_bls_verify_batch_device", "cess_bls_public_key_batch",
     "cess_bls_sign_batch", "cess_bls_hash_to_g1_batch", "cess_bls_gt_batch", "cess_bls_stage_times",
     "cess_bls_status_string", "cess_bls_version",
+    "cess_bls_verify_batch_rlc", "cess_bls_rlc_begin", "cess_bls_gt_product_is_one", "cess_bls_rlc_finish",
 )
 
 
@@ -81,6 +82,10 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_sign_batch.argtypes = [vp, sz, _u8p, _u8p, _u64p, _u8p]
         lib.cess_bls_hash_to_g1_batch.argtypes = [vp, sz, _u8p, _u64p, _u8p]
         lib.cess_bls_gt_batch.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p]
+        lib.cess_bls_rlc_begin.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p]
+        lib.cess_bls_gt_product_is_one.argtypes = [vp, sz, _u8p, ctypes.POINTER(ctypes.c_int)]
+        lib.cess_bls_rlc_finish.argtypes = [vp, ctypes.c_int, _u8p, _u64p, _u64p]
+        lib.cess_bls_verify_batch_rlc.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p, _u64p, _u64p]
         lib.cess_bls_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                              ctypes.c_int, ctypes.c_int]
         lib.cess_bls_status_string.restype = ctypes.c_char_p
@@ -189,6 +194,53 @@ class Context:
         """Device-resident batch (HBM pointers as ints); enqueued on `stream`, not synchronised."""
         self._chk(self._lib.cess_bls_verify_batch_device(self._h, n, d_sigs, d_pks, d_msgs, d_offs, d_codes,
                                                          d_bitmap, stream or None))
+
+    # --- RLC batch mode (random linear combination + bisection) ----------
+    def rlc_begin(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: bytes) -> bytes:
+        """Decode, hash and scale a fixed-stride batch, run its RLC check and
+        return this shard's Gt partial (576 canonical bytes).  The buffers are
+        kept alive until rlc_finish."""
+        n = len(sigs) // 48
+        assert len(sigs) == 48 * n and len(pks) == 96 * n and len(seed) == 32
+        keep = (_buf(sigs), _buf(pks), _buf(msgs), (ctypes.c_uint64 * (n + 1))(*msg_offsets), _buf(seed))
+        self._rlc_keep = keep
+        self._rlc_n = n
+        gt = (ctypes.c_uint8 * 576)()
+        self._chk(self._lib.cess_bls_rlc_begin(self._h, n, keep[0], keep[1], keep[2], keep[3], keep[4], gt))
+        return bytes(gt)
+
+    def gt_product_is_one(self, gts: bytes) -> bool:
+        """prod of m canonical Gt values (m*576 bytes) == 1, computed on the device."""
+        m = len(gts) // 576
+        ok = ctypes.c_int()
+        self._chk(self._lib.cess_bls_gt_product_is_one(self._h, m, _buf(gts), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def rlc_finish(self, global_ok: bool):
+        """Per-record codes of the batch given the (cross-shard) verdict of the
+        combined check; a failing shard is bisected.  -> (codes, bitmap, stats)"""
+        n = self._rlc_n
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        st = (ctypes.c_uint64 * 4)()
+        self._chk(self._lib.cess_bls_rlc_finish(self._h, 1 if global_ok else 0, codes, bitmap, st))
+        self._rlc_keep = None
+        stats = {"checks": st[0], "leaves": st[1], "leaf_sigs": st[2], "distinct_keys": st[3]}
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64], stats
+
+    def verify_rlc(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: Optional[bytes] = None):
+        """Single-GPU RLC batch verification -> (codes, bitmap, stats); codes equal
+        verify_fixed's (soundness error 2^-127 per check)."""
+        n = len(sigs) // 48
+        seed = seed if seed is not None else secrets.token_bytes(32)
+        offs = (ctypes.c_uint64 * (n + 1))(*msg_offsets)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        st = (ctypes.c_uint64 * 4)()
+        self._chk(self._lib.cess_bls_verify_batch_rlc(self._h, n, _buf(sigs), _buf(pks), _buf(msgs), offs,
+                                                      _buf(seed), codes, bitmap, st))
+        stats = {"checks": st[0], "leaves": st[1], "leaf_sigs": st[2], "distinct_keys": st[3]}
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64], stats
 
     # --- generator side -------------------------------------------------
     def public_keys(self, sks: Sequence[bytes]) -> list:

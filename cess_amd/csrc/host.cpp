@@ -8,6 +8,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cess_bls.h"
@@ -25,6 +27,14 @@ __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*,
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
 __global__ void k_hash_out(uint64_t, const uint8_t*, const uint64_t*, uint8_t*);
+// RLC batch mode (k_rlc.hip)
+__global__ void k_rlc_scale(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                            uint64_t, uint32_t*, uint32_t*, uint64_t, uint64_t);
+__global__ void k_g1_sum(uint64_t, const uint32_t*, uint64_t, const uint32_t*, uint64_t, uint32_t*, uint64_t);
+__global__ void k_rlc_pairs(uint32_t, const uint32_t*, const uint32_t*, uint64_t, const uint8_t*, uint8_t*, uint8_t*,
+                            uint32_t*, uint32_t*);
+__global__ void k_fp12_prod(uint32_t, const uint4*, uint64_t, uint4*);
+__global__ void k_gt_prod(uint32_t, const uint8_t*, uint4*, uint8_t*);
 
 namespace {
 
@@ -53,6 +63,21 @@ struct DevBuf {
   }
 };
 
+// State of one RLC batch between cess_bls_rlc_begin and cess_bls_rlc_finish.
+struct RlcState {
+  uint64_t n = 0;
+  const uint8_t *sigs = nullptr, *pks = nullptr, *msgs = nullptr;   // caller's records (kept valid by the caller)
+  const uint64_t* offs = nullptr;
+  std::vector<uint8_t> codes;       // decode codes; 0 = candidate for the pairing check
+  std::vector<uint32_t> perm;       // record indices sorted by key group
+  std::vector<uint64_t> gbeg;       // K + 1 group boundaries in perm
+  uint32_t K = 0;
+  bool local_ok = false;
+  uint64_t checks = 0, leaves = 0, leaf_sigs = 0;
+  DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
+  DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, acc, slots, fin_code, fin_bm, gt, gts, tmp;
+};
+
 }  // namespace
 
 struct cess_bls_ctx {
@@ -68,6 +93,7 @@ struct cess_bls_ctx {
   // profiling
   hipEvent_t ev[ST_N + 1] = {};
   double stage_ms[ST_N] = {};
+  RlcState* rlc = nullptr;
 };
 
 #define HIPCHK(x)                          \
@@ -175,6 +201,7 @@ extern "C" void cess_bls_ctx_destroy(cess_bls_ctx* c) {
   for (int i = 0; i <= ST_N; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c->rlc;
   delete c;
 }
 
@@ -396,4 +423,295 @@ extern "C" int cess_bls_stage_times(cess_bls_ctx* c, const char** names, double*
   if (reset)
     for (int i = 0; i < ST_N; i++) c->stage_ms[i] = 0;
   return ST_N;
+}
+
+// ---------------------------------------------------------------------------
+// RLC batch mode (north_star).  One random linear
+// combination per (sub)batch; on failure the batch is bisected down to leaves
+// of kRlcLeaf records, which are verified per signature, so the final codes are
+// those of cess_bls_verify_batch (up to the 2^-127 soundness error).
+// ---------------------------------------------------------------------------
+static constexpr uint64_t kRlcLeaf = 2048;
+
+// out (stride out_stride) = sum of in[perm[off + j]], j < cnt  (two passes)
+static int rlc_sum(cess_bls_ctx* c, RlcState& R, hipStream_t s, uint64_t off, uint64_t cnt, const uint32_t* in,
+                   uint64_t in_stride, uint32_t* out, uint64_t out_stride) {
+  uint64_t B = std::min<uint64_t>(1024, std::max<uint64_t>(1, (cnt + 255) / 256));
+  if (R.part.ensure(B * 36 * 4)) return CESS_BLS_E_OOM;
+  hipLaunchKernelGGL(k_g1_sum, dim3((unsigned)B), dim3(256), 0, s, cnt, R.d_perm.as<uint32_t>(), off, in, in_stride,
+                     R.part.as<uint32_t>(), B);
+  hipLaunchKernelGGL(k_g1_sum, dim3(1), dim3(256), 0, s, B, (const uint32_t*)nullptr, (uint64_t)0,
+                     (const uint32_t*)R.part.as<uint32_t>(), B, out, out_stride);
+  HIPCHK(hipGetLastError());
+  return CESS_BLS_OK;
+}
+
+// one RLC check over perm positions [a, b): *ok = product of the K+1 pairings
+// is 1; gt_out (optional) receives the Gt value (576 canonical bytes)
+static int rlc_check(cess_bls_ctx* c, RlcState& R, uint64_t a, uint64_t b, bool* ok, uint8_t* gt_out) {
+  hipStream_t s = c->stream;
+  const uint32_t K = R.K;
+  R.checks++;
+  int r = rlc_sum(c, R, s, a, b - a, R.P.as<uint32_t>(), R.n, R.S.as<uint32_t>(), 1);
+  if (r) return r;
+  for (uint32_t g = 0; g < K; g++) {
+    uint64_t lo = std::max(a, R.gbeg[g]), hi = std::min(b, R.gbeg[g + 1]);
+    r = rlc_sum(c, R, s, lo, hi > lo ? hi - lo : 0, R.Q.as<uint32_t>(), R.n, R.Qs.as<uint32_t>() + g, K);
+    if (r) return r;
+  }
+  hipLaunchKernelGGL(k_rlc_pairs, dim3((K + 63) / 64), dim3(64), 0, s, K, (const uint32_t*)R.S.as<uint32_t>(),
+                     (const uint32_t*)R.Qs.as<uint32_t>(), (uint64_t)K, (const uint8_t*)R.pk_usable.as<uint8_t>(),
+                     R.rec_code.as<uint8_t>(), R.rec_inf.as<uint8_t>(), R.rec_sig.as<uint32_t>(), R.rec_h.as<uint32_t>());
+  hipLaunchKernelGGL(k_miller, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, s, (uint64_t)K,
+                     (const uint8_t*)R.rec_code.as<uint8_t>(), (const uint8_t*)R.rec_inf.as<uint8_t>(),
+                     (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)R.pk_coeffs.as<uint4>(), R.rec_f.as<uint4>(),
+                     (uint64_t)K);
+  hipLaunchKernelGGL(k_fp12_prod, dim3(1), dim3(64), 0, s, K, (const uint4*)R.rec_f.as<uint4>(), (uint64_t)K,
+                     R.acc.as<uint4>());
+  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, 1, s));
+  hipLaunchKernelGGL(k_final, dim3(1), dim3(kBlock), 0, s, (uint64_t)1, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
+                     R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(), R.gt.as<uint8_t>(), (uint64_t)1);
+  HIPCHK(hipGetLastError());
+  uint8_t code = 0xff;
+  HIPCHK(hipMemcpyAsync(&code, R.fin_code.p, 1, hipMemcpyDeviceToHost, s));
+  if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *ok = code == CODE_OK;
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                  const uint8_t* msgs, const uint64_t* offs, const uint8_t* seed32, uint8_t* gt_out) {
+  if (!c || !seed32 || (n && (!sigs || !pks || !offs || (!msgs && offs[n] != offs[0])))) return CESS_BLS_E_INVALID_ARG;
+  if (n >= (1ull << 32)) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->rlc) c->rlc = new RlcState();
+  RlcState& R = *c->rlc;
+  R.n = n, R.sigs = sigs, R.pks = pks, R.msgs = msgs, R.offs = offs;
+  R.checks = R.leaves = R.leaf_sigs = 0;
+  R.codes.assign(n, 0);
+  R.local_ok = true;
+  if (n == 0) {
+    if (gt_out) {   // the empty product: Gt one
+      memset(gt_out, 0, 576);
+      gt_out[47] = 1;
+    }
+    R.K = 0;
+    return CESS_BLS_OK;
+  }
+  hipStream_t s = c->stream;
+  // 1. key groups (dedup of the 96-byte encodings) and a counting sort by group
+  std::unordered_map<std::string, uint32_t> groups;
+  std::vector<uint32_t> grp(n);
+  std::vector<uint64_t> first;
+  for (uint64_t i = 0; i < n; i++) {
+    auto it = groups.emplace(std::string((const char*)pks + 96 * i, 96), (uint32_t)first.size());
+    if (it.second) first.push_back(i);
+    grp[i] = it.first->second;
+  }
+  const uint32_t K = R.K = (uint32_t)first.size();
+  R.gbeg.assign(K + 1, 0);
+  for (uint64_t i = 0; i < n; i++) R.gbeg[grp[i] + 1]++;
+  for (uint32_t g = 0; g < K; g++) R.gbeg[g + 1] += R.gbeg[g];
+  R.perm.resize(n);
+  {
+    std::vector<uint64_t> pos(R.gbeg.begin(), R.gbeg.end() - 1);
+    for (uint64_t i = 0; i < n; i++) R.perm[pos[grp[i]]++] = (uint32_t)i;
+  }
+  // 2. device buffers
+  int r = 0;
+  r |= R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4) | R.d_perm.ensure(n * 4) | R.d_seed.ensure(32);
+  r |= R.S.ensure(36 * 4) | R.Qs.ensure((uint64_t)K * 36 * 4) | R.pk_in.ensure((uint64_t)K * 96);
+  r |= R.pk_code.ensure(K) | R.pk_inf.ensure(K) | R.pk_aff.ensure((uint64_t)K * CESS_W_G2 * 4);
+  r |= R.pk_coeffs.ensure((uint64_t)K * CESS_W_COEFFS * 4) | R.pk_usable.ensure(K);
+  r |= R.rec_code.ensure(K) | R.rec_inf.ensure(K) | R.rec_sig.ensure((uint64_t)K * CESS_W_G1 * 4);
+  r |= R.rec_h.ensure((uint64_t)K * CESS_W_G1 * 4) | R.rec_f.ensure((uint64_t)K * CESS_W_FP12 * 4);
+  r |= R.acc.ensure(CESS_W_FP12 * 4) | R.slots.ensure(CESS_W_FP12 * 4 * CESS_FE_SLOTS) | R.fin_code.ensure(1);
+  r |= R.fin_bm.ensure(8) | R.gt.ensure(576);
+  if (r) return CESS_BLS_E_OOM;
+  {
+    uint32_t sw[8];
+    for (int w = 0; w < 8; w++)
+      sw[w] = ((uint32_t)seed32[4 * w] << 24) | ((uint32_t)seed32[4 * w + 1] << 16) | ((uint32_t)seed32[4 * w + 2] << 8) |
+              seed32[4 * w + 3];
+    HIPCHK(hipMemcpyAsync(R.d_seed.p, sw, 32, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipMemcpyAsync(R.d_perm.p, R.perm.data(), n * 4, hipMemcpyHostToDevice, s));
+  // 3. distinct keys: decode (G2Affine::from_compressed, src/lib.rs:74) + G2Prepared (:88), once per key
+  std::vector<uint8_t> kbytes((uint64_t)K * 96), pkc(K), pki(K), usable(K);
+  for (uint32_t g = 0; g < K; g++) memcpy(&kbytes[96 * (uint64_t)g], pks + 96 * first[g], 96);
+  HIPCHK(hipMemcpyAsync(R.pk_in.p, kbytes.data(), kbytes.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(R.pk_code.p, 0, K, s));
+  HIPCHK(hipMemsetAsync(R.pk_inf.p, 0, K, s));
+  hipLaunchKernelGGL(k_decode_pk, dim3(grid_for(K)), dim3(kBlock), 0, s, (uint64_t)K, R.pk_in.as<uint8_t>(),
+                     (const uint8_t*)nullptr, R.pk_code.as<uint8_t>(), R.pk_inf.as<uint8_t>(), R.pk_aff.as<uint32_t>(),
+                     (uint64_t)K);
+  hipLaunchKernelGGL(k_prepare, dim3(grid_for(K)), dim3(kBlock), 0, s, (uint64_t)K,
+                     (const uint32_t*)R.pk_aff.as<uint32_t>(), R.pk_coeffs.as<uint4>(), (uint64_t)K);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(pkc.data(), R.pk_code.p, K, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(pki.data(), R.pk_inf.p, K, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint32_t g = 0; g < K; g++) usable[g] = pkc[g] == 0 && !(pki[g] & INF_PK);
+  HIPCHK(hipMemcpyAsync(R.pk_usable.p, usable.data(), K, hipMemcpyHostToDevice, s));
+  // 4. per chunk: decode sig (src/lib.rs:144), key codes in reference precedence
+  //    (signature first, :244-245), hash_to_g1 (:25-31), P_i = r_i sig_i, Q_i = r_i H_i
+  std::vector<uint8_t> hc, hi;
+  std::vector<uint64_t> rebased;
+  for (uint64_t off = 0; off < n; off += c->cap) {
+    const uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    const uint64_t mb0 = offs[off], mb1 = offs[off + m];
+    rebased.resize(m + 1);
+    for (uint64_t j = 0; j <= m; j++) {
+      if (j && offs[off + j] < offs[off + j - 1]) return CESS_BLS_E_INVALID_ARG;
+      rebased[j] = offs[off + j] - mb0;
+    }
+    r = c->in_sigs.ensure(m * 48) | c->in_msgs.ensure(std::max<uint64_t>(mb1 - mb0, 1)) | c->in_offs.ensure((m + 1) * 8);
+    if (r) return CESS_BLS_E_OOM;
+    HIPCHK(hipMemcpyAsync(c->in_sigs.p, sigs + 48 * off, m * 48, hipMemcpyHostToDevice, s));
+    if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+    const unsigned g = grid_for(m);
+    hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
+                       c->code.as<uint8_t>(), c->inf.as<uint8_t>(), c->sig_aff.as<uint32_t>(), c->cap);
+    HIPCHK(hipGetLastError());
+    hc.resize(m);
+    hi.resize(m);
+    HIPCHK(hipMemcpyAsync(hc.data(), c->code.p, m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hi.data(), c->inf.p, m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (uint64_t j = 0; j < m; j++) {
+      if (hc[j] != 0) continue;
+      const uint32_t gg = grp[off + j];
+      if (pkc[gg] != 0) hc[j] = pkc[gg];
+      else if (pki[gg] & INF_PK) hi[j] |= INF_PK;
+    }
+    memcpy(&R.codes[off], hc.data(), m);
+    HIPCHK(hipMemcpyAsync(c->code.p, hc.data(), m, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->inf.p, hi.data(), m, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
+                       (const uint8_t*)c->code.as<uint8_t>(), c->h_aff.as<uint32_t>(), c->cap);
+    hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)c->code.as<uint8_t>(),
+                       (const uint8_t*)c->inf.as<uint8_t>(), (const uint32_t*)c->sig_aff.as<uint32_t>(),
+                       (const uint32_t*)c->h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(), off,
+                       R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->cap, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // hc/hi are reused by the next chunk
+  }
+  // 5. the batch check (this shard's Gt partial)
+  bool ok = false;
+  r = rlc_check(c, R, 0, n, &ok, gt_out);
+  if (r) return r;
+  R.local_ok = ok;
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_gt_product_is_one(cess_bls_ctx* c, size_t m, const uint8_t* gts, int* is_one) {
+  if (!c || !is_one || (m && !gts)) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->rlc) c->rlc = new RlcState();
+  RlcState& R = *c->rlc;
+  if (m == 0) {
+    *is_one = 1;
+    return CESS_BLS_OK;
+  }
+  hipStream_t s = c->stream;
+  if (R.gts.ensure(m * 576) | R.tmp.ensure(2 * CESS_W_FP12 * 4) | R.fin_code.ensure(1)) return CESS_BLS_E_OOM;
+  HIPCHK(hipMemcpyAsync(R.gts.p, gts, m * 576, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_gt_prod, dim3(1), dim3(64), 0, s, (uint32_t)m, (const uint8_t*)R.gts.as<uint8_t>(),
+                     R.tmp.as<uint4>(), R.fin_code.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  uint8_t code = 0xff;
+  HIPCHK(hipMemcpyAsync(&code, R.fin_code.p, 1, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *is_one = code == CODE_OK;
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_rlc_finish(cess_bls_ctx* c, int global_ok, uint8_t* codes_out, uint64_t* bitmap_out,
+                                   uint64_t* stats4) {
+  if (!c || !c->rlc) return CESS_BLS_E_INVALID_ARG;
+  RlcState& R = *c->rlc;
+  const uint64_t n = R.n;
+  std::vector<uint8_t>& codes = R.codes;
+  if (!global_ok && !R.local_ok) {
+    // bisection over perm positions; `known` = this range is known to fail
+    struct Rg {
+      uint64_t a, b;
+      bool known;
+    };
+    std::vector<Rg> work = {{0, n, true}};
+    std::vector<uint8_t> ls, lp, lm, lc;
+    std::vector<uint64_t> lo, li;
+    while (!work.empty()) {
+      Rg w = work.back();
+      work.pop_back();
+      if (w.b - w.a <= kRlcLeaf) {
+        // leaf: per-signature verification of the candidates (exact codes)
+        li.clear();
+        for (uint64_t j = w.a; j < w.b; j++)
+          if (codes[R.perm[j]] == 0) li.push_back(R.perm[j]);
+        if (li.empty()) continue;
+        const uint64_t m = li.size();
+        ls.resize(m * 48);
+        lp.resize(m * 96);
+        lm.clear();
+        lo.assign(1, 0);
+        for (uint64_t q = 0; q < m; q++) {
+          const uint64_t i = li[q];
+          memcpy(&ls[48 * q], R.sigs + 48 * i, 48);
+          memcpy(&lp[96 * q], R.pks + 96 * i, 96);
+          lm.insert(lm.end(), R.msgs + R.offs[i], R.msgs + R.offs[i + 1]);
+          lo.push_back(lm.size());
+        }
+        lc.resize(m);
+        int r = verify_host(c, m, ls.data(), lp.data(), lm.empty() ? nullptr : lm.data(), lo.data(), nullptr,
+                            lc.data(), nullptr, nullptr);
+        if (r) return r;
+        for (uint64_t q = 0; q < m; q++) codes[li[q]] = lc[q];
+        R.leaves++;
+        R.leaf_sigs += m;
+        continue;
+      }
+      bool ok = false;
+      if (!w.known) {
+        int r = rlc_check(c, R, w.a, w.b, &ok, nullptr);
+        if (r) return r;
+        if (ok) continue;
+      }
+      const uint64_t mid = w.a + (w.b - w.a) / 2;
+      // check the left half first; if it passes, the right half must fail
+      bool left_ok = false;
+      if (mid - w.a > kRlcLeaf) {
+        int r = rlc_check(c, R, w.a, mid, &left_ok, nullptr);
+        if (r) return r;
+        if (!left_ok) work.push_back({w.a, mid, true});
+      } else {
+        work.push_back({w.a, mid, true});
+      }
+      work.push_back({mid, w.b, left_ok});
+    }
+  }
+  if (codes_out) memcpy(codes_out, codes.data(), n);
+  if (bitmap_out) {
+    for (uint64_t w = 0; w < (n + 63) / 64; w++) bitmap_out[w] = 0;
+    for (uint64_t i = 0; i < n; i++)
+      if (codes[i] == 0) bitmap_out[i >> 6] |= 1ull << (i & 63);
+  }
+  if (stats4) {
+    stats4[0] = R.checks;
+    stats4[1] = R.leaves;
+    stats4[2] = R.leaf_sigs;
+    stats4[3] = R.K;
+  }
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_verify_batch_rlc(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                         const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
+                                         uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4) {
+  int r = cess_bls_rlc_begin(c, n, sigs, pks, msgs, msg_offsets, seed32, nullptr);
+  if (r) return r;
+  return cess_bls_rlc_finish(c, c->rlc->local_ok, codes_out, bitmap_out, stats4);
 }

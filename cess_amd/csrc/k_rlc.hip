@@ -1,0 +1,175 @@
+// CDNA4 (gfx950) kernels of the random-linear-combination (RLC) batch mode
+// (BASELINE north_star "optional random-linear-combination batch mode"; SURVEY
+// §8(d) C4 / §8(e)).  For a (sub)batch with distinct keys pk_1..pk_K:
+//
+//   e(sum_i r_i sig_i, -G2) * prod_k e(sum_{i: pk_i = pk_k} r_i H(m_i), pk_k) == 1
+//
+// holds iff every member passes verify_bls_signature's pairing equation
+// (src/lib.rs:85-100), except with probability <= 2^-127 over the 128-bit r_i.
+// Malformed encodings never enter the sums: they keep their decode codes.
+//
+// k_rlc_scale  : P_i = r_i sig_i, Q_i = r_i H(m_i)   (r_i = SHA-256(seed || i)[0:16] | 1)
+// k_g1_sum     : sum of projective G1 points over a (permuted) index range
+// k_rlc_pairs  : K+1 summed points -> affine Miller-loop records (k_miller input)
+// k_fp12_prod  : product of m Miller-loop values (one lane)
+// k_gt_prod    : product of m canonical Gt values == 1 ?  (cross-rank combine)
+#include <hip/hip_runtime.h>
+#include "soa.hpp"
+
+using namespace bls;
+using namespace cess;
+
+namespace {
+
+// projective G1 in SoA: x at words 0..11, y 12..23, z 24..35
+__device__ __forceinline__ g1p ld_g1p(const uint32_t* b, uint64_t stride, uint32_t i) {
+  return {ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), ld_fp(b + 24 * stride, stride, i)};
+}
+__device__ __forceinline__ void st_g1p(uint32_t* b, uint64_t stride, uint32_t i, const g1p& p) {
+  st_fp(b, stride, i, p.x);
+  st_fp(b + 12 * stride, stride, i, p.y);
+  st_fp(b + 24 * stride, stride, i, p.z);
+}
+
+// 128-bit scalar of record i from the batch seed (8 big-endian words)
+__device__ void rlc_scalar(const uint32_t* seed, uint64_t i, uint32_t (&k)[4]) {
+  uint32_t blk[16], st[8];
+#pragma unroll
+  for (int w = 0; w < 8; w++) blk[w] = seed[w], st[w] = SHA_IV[w];
+  blk[8] = (uint32_t)(i >> 32);
+  blk[9] = (uint32_t)i;
+  blk[10] = 0x80000000u;
+#pragma unroll
+  for (int w = 11; w < 15; w++) blk[w] = 0;
+  blk[15] = 320;   // 40-byte message
+  sha256_compress(st, blk);
+#pragma unroll
+  for (int w = 0; w < 4; w++) k[w] = st[w];
+  k[0] |= 1u;      // nonzero
+}
+
+}  // namespace
+
+__global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                    const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
+                                    const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
+                                    uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1p p = proj_identity<fp>(), q = proj_identity<fp>();
+  const uint8_t fl = inf[i];
+  if (code[i] == 0) {
+    uint32_t k[4];
+    rlc_scalar(seed, index_base + i, k);
+    const bool use_s = (fl & INF_SIG) == 0, use_h = (fl & INF_PK) == 0;
+    fp sx = ld_fp(sig_aff, stride, i), sy = ld_fp(sig_aff + 12 * stride, stride, i);
+    fp hx = ld_fp(h_aff, stride, i), hy = ld_fp(h_aff + 12 * stride, stride, i);
+#pragma unroll 1
+    for (int w = 3; w >= 0; w--) {
+#pragma unroll 1
+      for (int b = 31; b >= 0; b--) {
+        if (use_s) p = proj_dbl(p);
+        if (use_h) q = proj_dbl(q);
+        if ((k[w] >> b) & 1u) {
+          if (use_s) p = proj_add_mixed(p, sx, sy);
+          if (use_h) q = proj_add_mixed(q, hx, hy);
+        }
+      }
+    }
+  }
+  st_g1p(P, out_stride, i, p);
+  st_g1p(Q, out_stride, i, q);
+}
+
+// out[blockIdx.x] = sum_{j < cnt} in[idx(j)], idx(j) = perm ? perm[off + j] : off + j
+__global__ __launch_bounds__(256, 1) void k_g1_sum(uint64_t cnt, const uint32_t* __restrict__ perm, uint64_t off,
+                                                   const uint32_t* __restrict__ in, uint64_t in_stride,
+                                                   uint32_t* __restrict__ out, uint64_t out_stride) {
+  __shared__ uint32_t L[36][256];
+  const uint32_t t = threadIdx.x;
+  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + t; j < cnt; j += T) {
+    const uint64_t idx = perm ? perm[off + j] : off + j;
+    acc = proj_add(acc, ld_g1p(in, in_stride, (uint32_t)idx));
+  }
+#pragma unroll 1
+  for (uint32_t s = 128; s >= 1; s >>= 1) {
+    if (t >= s && t < 2 * s) {
+      const fp* e = &acc.x;
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+#pragma unroll
+        for (int l = 0; l < 12; l++) L[12 * w + l][t - s] = e[w].v[l];
+    }
+    __syncthreads();
+    if (t < s) {
+      g1p o;
+      fp* e = &o.x;
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+#pragma unroll
+        for (int l = 0; l < 12; l++) e[w].v[l] = L[12 * w + l][t];
+      acc = proj_add(acc, o);
+    }
+    __syncthreads();
+  }
+  if (t == 0) st_g1p(out, out_stride, blockIdx.x, acc);
+}
+
+// Records j < m of the K+1-pair check: pair 0 carries S (record 0 only),
+// pair 1 carries (Q_j, pk_j).  pk_usable[j] = 0 for keys that are the identity
+// (their pairing term is 1).  Output in k_miller's SoA input format (stride m).
+__global__ void k_rlc_pairs(uint32_t m, const uint32_t* __restrict__ S, const uint32_t* __restrict__ Qs,
+                            uint64_t q_stride, const uint8_t* __restrict__ pk_usable, uint8_t* __restrict__ code,
+                            uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff, uint32_t* __restrict__ h_aff) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  uint8_t f = 0;
+  g1a s = {fp_zero(), fp_one(), true};
+  if (j == 0) s = proj_to_affine(ld_g1p(S, 1, 0));
+  if (s.inf) f |= INF_SIG;
+  g1a h = proj_to_affine(ld_g1p(Qs, q_stride, j));
+  if (h.inf || !pk_usable[j]) f |= INF_PK;
+  st_fp(sig_aff, m, j, s.x);
+  st_fp(sig_aff + 12 * m, m, j, s.y);
+  st_fp(h_aff, m, j, h.x);
+  st_fp(h_aff + 12 * m, m, j, h.y);
+  inf[j] = f;
+  code[j] = 0;
+}
+
+// acc (stride-1 slot) = prod_{j < m} fin[j]  (fin: uint4 SoA with stride fstride)
+__global__ void k_fp12_prod(uint32_t m, const uint4* __restrict__ fin, uint64_t fstride, uint4* __restrict__ acc) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  GlobF12 a{acc, 1, 0};
+  copy12(a, GlobF12{const_cast<uint4*>(fin), fstride, 0});
+#pragma unroll 1
+  for (uint32_t j = 1; j < m; j++) mul12(a, GlobF12{const_cast<uint4*>(fin), fstride, j});
+}
+
+// code[0] = 0 iff prod_{j < m} gt_j == 1; gts: m canonical Gt values (576 B,
+// 12 big-endian Fp in tower order, the cess_bls_gt_batch format)
+__global__ void k_gt_prod(uint32_t m, const uint8_t* __restrict__ gts, uint4* __restrict__ tmp,
+                          uint8_t* __restrict__ code) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  GlobF12 a{tmp, 1, 0}, b{tmp + 36, 1, 0};
+#pragma unroll 1
+  for (uint32_t j = 0; j < m; j++) {
+    const GlobF12& d = j ? b : a;
+#pragma unroll 1
+    for (int k = 0; k < 6; k++) {
+      uint32_t w[24];
+      const uint8_t* src = gts + 576 * (uint64_t)j + 96 * k;
+#pragma unroll 1
+      for (int t = 0; t < 24; t++)
+        w[t] = ((uint32_t)src[4 * t] << 24) | ((uint32_t)src[4 * t + 1] << 16) | ((uint32_t)src[4 * t + 2] << 8) |
+               src[4 * t + 3];
+      fp2 e = {to_mont(raw_from_be_words(w)), to_mont(raw_from_be_words(w + 12))};
+      d.st(k, e);
+    }
+    if (j) mul12(a, b);
+  }
+  code[0] = is_one12(a) ? CODE_OK : CODE_PAIRING;
+}

@@ -114,6 +114,30 @@ int cess_bls_hash_to_g1_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* msgs, 
 int cess_bls_gt_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
                       const uint64_t* msg_offsets, uint8_t* codes_out, uint8_t* gt_out);
 
+/* ---- RLC batch mode (north_star "optional random-linear-combination batch
+ * mode"; no reference counterpart).  For records with distinct keys
+ * pk_1..pk_K, one check
+ *     e(sum r_i sig_i, -G2) * prod_k e(sum_{pk_i = pk_k} r_i H(m_i), pk_k) == 1
+ * (r_i: 128-bit, derived from `seed32` by SHA-256) replaces n pairing
+ * products; a failing batch is bisected down to leaves verified per signature,
+ * so codes_out equals cess_bls_verify_batch's except with probability 2^-127
+ * per check.  Fixed-stride records (48-B sigs, 96-B keys), host buffers. */
+int cess_bls_verify_batch_rlc(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                              const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
+                              uint8_t* codes_out, uint64_t* bitmap_out,
+                              uint64_t* stats4 /* checks, leaves, leaf sigs, distinct keys; may be NULL */);
+
+/* Multi-GPU form (one shard per context): rlc_begin runs the shard's check and
+ * returns its Gt partial (576 canonical bytes); the caller all-gathers the
+ * partials (RCCL), combines them with cess_bls_gt_product_is_one, and passes
+ * the global verdict to rlc_finish, which bisects the shard if needed.  The
+ * record buffers must stay valid until rlc_finish returns. */
+int cess_bls_rlc_begin(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                       const uint64_t* msg_offsets, const uint8_t* seed32, uint8_t* gt_out);
+int cess_bls_gt_product_is_one(cess_bls_ctx* ctx, size_t m, const uint8_t* gts, int* is_one);
+int cess_bls_rlc_finish(cess_bls_ctx* ctx, int global_ok, uint8_t* codes_out, uint64_t* bitmap_out,
+                        uint64_t* stats4);
+
 /* Per-stage timings (ms, summed since the last reset) when CESS_BLS_F_PROFILE is
  * set.  names/ms arrays of length max; returns the number of stages. */
 int cess_bls_stage_times(cess_bls_ctx* ctx, const char** names, double* ms, int max, int reset);

@@ -1,0 +1,98 @@
+"""GPU: RLC batch mode (random linear combination + bisection, BASELINE config
+4 shape: few keys).  Parity bar: the per-record codes equal the per-signature
+path's (cess_bls_verify_batch) on the same records, including forged,
+malformed, non-subgroup and identity inputs, and the cross-shard Gt-product
+combine gives the same verdicts as one shard."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _few_key_batch(ctx, n, nkeys, seed):
+    rng = random.Random(seed)
+    sks = [rng.randrange(1, R).to_bytes(32, "big") for _ in range(nkeys)]
+    pks = ctx.public_keys(sks)
+    owner = [rng.randrange(nkeys) for _ in range(n)]
+    msgs = [rng.randbytes(32) for _ in range(n)]
+    sigs = ctx.sign([sks[o] for o in owner], msgs)
+    return sigs, [pks[o] for o in owner], msgs
+
+
+def _pack(sigs, pks, msgs):
+    offs = [0]
+    for m in msgs:
+        offs.append(offs[-1] + len(m))
+    return b"".join(sigs), b"".join(pks), b"".join(msgs), offs
+
+
+def test_rlc_all_valid_single_check(ctx):
+    sigs, pks, msgs = _few_key_batch(ctx, 3000, 5, 1)
+    codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(range(32)))
+    assert set(codes) == {0}
+    assert st["checks"] == 1 and st["leaves"] == 0 and st["distinct_keys"] == 5
+    assert words[:3000 // 64] == [(1 << 64) - 1] * (3000 // 64)
+
+
+def test_rlc_codes_equal_per_signature_path(ctx, vectors):
+    """Forgeries, bad encodings and the golden adversarial cases spread over a
+    9,000-record batch: bisection must isolate them with exact codes."""
+    sigs, pks, msgs = _few_key_batch(ctx, 9000, 7, 2)
+    rng = random.Random(3)
+    idx = rng.sample(range(9000), 12)
+    # forged: valid signature over another message
+    msgs[idx[0]] = rng.randbytes(32)
+    msgs[idx[1]] = msgs[idx[1]][:31] + bytes([msgs[idx[1]][31] ^ 1])
+    # signature of another record (valid point, wrong pairing)
+    sigs[idx[2]] = sigs[idx[3]]
+    # malformed signature encodings
+    sigs[idx[4]] = bytes([sigs[idx[4]][0] & 0x7F]) + sigs[idx[4]][1:]          # compression bit clear
+    sigs[idx[5]] = b"\xc0" + bytes(47)                                         # identity signature
+    # golden adversarial records (non-subgroup sig, off-curve key, x >= p, ...)
+    cases = [c for c in vectors["cases"] if len(bytes.fromhex(c["sig"])) == 48 and len(bytes.fromhex(c["pk"])) == 96]
+    for j, c in zip(idx[6:], cases[:6]):
+        sigs[j], msgs[j], pks[j] = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+    S, P, M, offs = _pack(sigs, pks, msgs)
+    expect, ewords = ctx.verify_fixed(S, P, M, offs)
+    codes, words, st = ctx.verify_rlc(S, P, M, offs, seed=bytes(32))
+    assert codes == expect
+    assert words == ewords
+    assert expect.count(0) < 9000 - 3
+    assert st["checks"] > 1 and st["leaves"] >= 1
+
+
+def test_rlc_cross_shard_combine(ctx):
+    """Two shards (two contexts, as two ranks would hold): the product of the
+    shards' Gt partials decides; only the failing shard bisects."""
+    from cess_amd import bls
+    sigs, pks, msgs = _few_key_batch(ctx, 6000, 4, 4)
+    msgs[4500] = bytes(32)          # one forgery, in shard 1
+    halves = [(0, 3000), (3000, 6000)]
+    ctxs = [ctx, bls.Context(max_batch=1 << 14)]
+    try:
+        gts = []
+        for c, (a, b) in zip(ctxs, halves):
+            gts.append(c.rlc_begin(*_pack(sigs[a:b], pks[a:b], msgs[a:b]), seed=bytes([a & 255]) * 32))
+        one = bytes(47) + b"\x01" + bytes(576 - 48)
+        assert gts[0] == one and gts[1] != one
+        ok = ctxs[0].gt_product_is_one(b"".join(gts))
+        assert not ok
+        assert ctxs[0].gt_product_is_one(gts[0] + gts[0])
+        res = [c.rlc_finish(ok) for c in ctxs]
+    finally:
+        ctxs[1].close()
+    assert set(res[0][0]) == {0} and res[0][2]["leaves"] == 0
+    c1 = res[1][0]
+    assert c1[1500] == 5 and c1.count(0) == 2999 and res[1][2]["leaves"] >= 1
+
+
+def test_rlc_empty_and_tiny(ctx):
+    codes, words, st = ctx.verify_rlc(b"", b"", b"", [0], seed=bytes(32))
+    assert codes == b"" and st["checks"] == 0
+    sigs, pks, msgs = _few_key_batch(ctx, 3, 1, 5)
+    msgs[1] = bytes(32)
+    codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(32))
+    assert list(codes) == [0, 5, 0]

@@ -8,8 +8,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/cess_bls.h"
@@ -501,14 +499,46 @@ extern "C" int cess_bls_rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs
     return CESS_BLS_OK;
   }
   hipStream_t s = c->stream;
-  // 1. key groups (dedup of the 96-byte encodings) and a counting sort by group
-  std::unordered_map<std::string, uint32_t> groups;
+  // 1. key groups (dedup of the 96-byte encodings; open addressing on a
+  //    64-bit hash, full compare) and a counting sort by group
   std::vector<uint32_t> grp(n);
   std::vector<uint64_t> first;
-  for (uint64_t i = 0; i < n; i++) {
-    auto it = groups.emplace(std::string((const char*)pks + 96 * i, 96), (uint32_t)first.size());
-    if (it.second) first.push_back(i);
-    grp[i] = it.first->second;
+  {
+    auto khash = [](const uint8_t* k) {
+      uint64_t h = 0x9E3779B97F4A7C15ull;
+      for (int q = 0; q < 96; q += 8) {
+        uint64_t w;
+        memcpy(&w, k + q, 8);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+      }
+      return h;
+    };
+    std::vector<uint32_t> slot(64, 0);   // group id + 1; 0 = empty
+    uint64_t mask = 63;
+    for (uint64_t i = 0; i < n; i++) {
+      const uint8_t* k = pks + 96 * i;
+      uint64_t h = khash(k) & mask;
+      while (slot[h] && memcmp(pks + 96 * first[slot[h] - 1], k, 96) != 0) h = (h + 1) & mask;
+      if (!slot[h]) {
+        first.push_back(i);
+        slot[h] = (uint32_t)first.size();
+        if (2 * first.size() > mask) {   // grow and rehash
+          std::vector<uint32_t> ns(2 * (mask + 1), 0);
+          const uint64_t nm = 2 * (mask + 1) - 1;
+          for (uint32_t g = 0; g < first.size(); g++) {
+            uint64_t q = khash(pks + 96 * first[g]) & nm;
+            while (ns[q]) q = (q + 1) & nm;
+            ns[q] = g + 1;
+          }
+          slot.swap(ns);
+          mask = nm;
+        }
+        grp[i] = (uint32_t)first.size() - 1;
+      } else {
+        grp[i] = slot[h] - 1;
+      }
+    }
   }
   const uint32_t K = R.K = (uint32_t)first.size();
   R.gbeg.assign(K + 1, 0);

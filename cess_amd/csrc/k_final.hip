@@ -13,16 +13,31 @@ using namespace cess;
 
 __constant__ uint8_t kFeProgram[][2] = {CESS_FE_PROGRAM};
 
-__global__ CESS_LB void k_final(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
-                                uint4* __restrict__ slots, uint64_t* __restrict__ bitmap,
-                                uint8_t* __restrict__ gt_out, uint64_t stride) {
-  __shared__ uint4 F[36][256];
+// Accumulator placement as in k_miller (CESS_FINAL_HBM): an eighth HBM slot
+// (two waves per SIMD) or the LDS image (one wave per SIMD).
+#ifndef CESS_FINAL_HBM
+#define CESS_FINAL_HBM 1
+#endif
+#if CESS_FINAL_HBM
+#define CESS_LB_F12 __launch_bounds__(256, 2)
+#else
+#define CESS_LB_F12 __launch_bounds__(256, 1)
+#endif
+
+__global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
+                                    uint4* __restrict__ slots, uint64_t* __restrict__ bitmap,
+                                    uint8_t* __restrict__ gt_out, uint64_t stride) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t c = CODE_SIG_LEN;
   if (i < n) {
     c = code[i];
     if (c == 0) {
+#if CESS_FINAL_HBM
+      GlobF12 acc{slots + (uint64_t)(SL_N - 1) * 36 * stride, stride, i};
+#else
+      __shared__ uint4 F[36][256];
       LdsF12 acc{F, threadIdx.x};
+#endif
       final_exp_staged(acc, kFeProgram, [&](int s) {
         return GlobF12{s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride, stride, i};
       });

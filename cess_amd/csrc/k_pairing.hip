@@ -18,18 +18,33 @@ __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_af
   g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); });
 }
 
-// LDS image of the 256 lanes' Miller accumulators: 144 dwords x 256 = 144 KiB
-__global__ CESS_LB void k_miller(uint64_t n, const uint8_t* __restrict__ code,
-                                 const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
-                                 const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
-                                 const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
-                                 uint64_t stride) {
-  __shared__ uint4 F[36][256];
+// Miller accumulator placement: CESS_MILLER_HBM=1 keeps each lane's Fp12 in its
+// HBM output slot (L2/MALL-resident) so two waves fit per SIMD; 0 keeps it in
+// an LDS image (144 dwords x 256 lanes = 144 KiB, one wave per SIMD).
+#ifndef CESS_MILLER_HBM
+#define CESS_MILLER_HBM 0
+#endif
+#if CESS_MILLER_HBM
+#define CESS_LB_F12 __launch_bounds__(256, 2)
+#else
+#define CESS_LB_F12 __launch_bounds__(256, 1)
+#endif
+
+__global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ code,
+                                     const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
+                                     const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
+                                     const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
+                                     uint64_t stride) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (code[i] != 0) return;
   uint8_t fl = inf[i];
+#if CESS_MILLER_HBM
+  GlobF12 f{fout, stride, i};
+#else
+  __shared__ uint4 F[36][256];
   LdsF12 f{F, threadIdx.x};
+#endif
   // the G1 points are re-read from HBM (L2) for every line instead of being
   // held in 48 registers across the loop
   miller_loop2_staged(
@@ -39,5 +54,7 @@ __global__ CESS_LB void k_miller(uint64_t n, const uint8_t* __restrict__ code,
         return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
       },
       [&](int pair, int k) { return pair ? ld_coeff4(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k); });
+#if !CESS_MILLER_HBM
   copy12(GlobF12{fout, stride, i}, f);
+#endif
 }

@@ -48,3 +48,36 @@ def gather_bitmap(local_words, n: int, world: int, group=None):
     else:
         dist.all_gather_into_tensor(out, buf, group=group)
     return torch.cat([out[r * mx: r * mx + sizes[r]] for r in range(world)])
+
+
+def shard_seed(seed: bytes, rank: int) -> bytes:
+    """Per-rank RLC seed.  The scalars r_i are derived from (seed, local index);
+    without a rank-specific seed two ranks would reuse the same r_i, letting an
+    adversary cancel errors across shards."""
+    import hashlib
+    return hashlib.sha256(b"cess-rlc-shard" + seed + rank.to_bytes(4, "little")).digest()
+
+
+def verify_rlc_sharded(ctx, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: bytes,
+                       rank: int, world: int, device=None, group=None):
+    """RLC batch mode across ranks: every rank checks its shard
+    and contributes its Gt partial; the partials are all-gathered (RCCL over
+    xGMI; gloo on CPU) and multiplied on the device; only a rank whose own
+    partial fails bisects.  Arguments are this rank's shard (fixed-stride
+    records); returns (codes, bitmap words, stats) for the shard."""
+    import torch
+    import torch.distributed as dist
+
+    gt = ctx.rlc_begin(sigs, pks, msgs, msg_offsets, shard_seed(seed, rank))
+    if world == 1:
+        gts = gt
+    else:
+        dev = device if device is not None else torch.device("cpu")
+        mine = torch.tensor(list(gt), dtype=torch.uint8, device=dev)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine, group=group)
+        gts = b"".join(bytes(p.cpu().tolist()) for p in parts)
+    ok = ctx.gt_product_is_one(gts)
+    codes, words, stats = ctx.rlc_finish(ok)
+    stats = dict(stats, global_ok=ok)
+    return codes, words, stats

@@ -70,3 +70,59 @@ def test_shard_ranges_cover_and_align():
                 assert a == prev and (a % 64 == 0 or a == n)
                 prev = b
             assert prev == n
+
+
+# --- RLC orchestration (cess_amd.dist.verify_rlc_sharded) ------------------
+GT_ONE = bytes(47) + b"\x01" + bytes(528)
+
+
+class _ShardCtx:
+    """Stand-in for a GPU context: a record is 'valid' iff its message byte 0
+    is even.  The Gt partial is one iff the shard is all valid (the algebra is
+    the GPU's; this checks the cross-rank protocol)."""
+
+    def rlc_begin(self, sigs, pks, msgs, offs, seed):
+        self.seed = seed
+        self.valid = [msgs[offs[i]] % 2 == 0 for i in range(len(offs) - 1)]
+        return GT_ONE if all(self.valid) else b"\x02" + bytes(575)
+
+    def gt_product_is_one(self, gts):
+        return all(gts[i:i + 576] == GT_ONE for i in range(0, len(gts), 576))
+
+    def rlc_finish(self, ok):
+        codes = bytes(0 if (ok or v) else 5 for v in self.valid)
+        return codes, [], {"checks": 1}
+
+
+def _rlc_worker(rank, world, port, n, bad, q):
+    from cess_amd.dist import verify_rlc_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = shard_range(n, rank, world)
+    msgs = bytes(1 if i in bad else 2 for i in range(a, b))
+    ctx = _ShardCtx()
+    codes, _, st = verify_rlc_sharded(ctx, b"", b"", msgs, list(range(b - a + 1)), b"s" * 32, rank, world)
+    q.put((rank, codes, st["global_ok"], ctx.seed))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad", [set(), {700}])
+def test_rlc_sharded_protocol(bad):
+    n, world = 1000, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rlc_worker, args=(r, world, port, n, bad, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, codes, ok, seed = q.get(timeout=120)
+        res[r] = (codes, ok, seed)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][2] != res[1][2]                      # per-rank scalars
+    assert all(res[r][1] == (not bad) for r in range(world))
+    full = res[0][0] + res[1][0]
+    assert [i for i in range(n) if full[i] != 0] == sorted(bad)

@@ -220,36 +220,30 @@ CESS_HD fp pack28(const uint32_t (&l)[14]) {
   return r;
 }
 
-// Montgomery multiplication, separated operand scanning (SOS).
-//
-// The 27 columns of the double-width product are first accumulated in 27
-// independent 64-bit accumulators (`prod(T)`), then reduced column by column:
-// m_k = T_k * (-p^-1) mod 2^28, T_{k..k+13} += m_k * p, carry T_k >> 28.  Only
-// the m_k -> carry -> m_{k+1} chain is serial; the 392 limb products are spread
-// over 27 accumulation chains, so one wave per SIMD keeps v_mad_u64_u32 issuing
-// instead of waiting on a single column accumulator (product scanning measured
-// ~3,850 cycles per multiply per wave on MI355X, latency-bound).
-// Column bound: 14 * 2^56 (a*b) + 14 * 2^56 (m*p) + 2^37 < 2^61.
-template <class Prod>
-CESS_HD fp mont28(Prod&& prod) {
-  uint64_t T[28];
-  prod(T);
-  T[27] = 0;
+// Montgomery reduction tail shared by mul and sqr:
+//   columns k of the double-width product are accumulated by `col(k, acc)`.
+template <class Col>
+CESS_HD fp mont28(Col&& col) {
+  uint32_t m[14], t[14];
+  uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 14; k++) {
-    const uint32_t m = ((uint32_t)T[k] * c::PINV28) & M28;
-    T[k] += (uint64_t)m * c::P28[0];
-    T[k + 1] += T[k] >> 28;
+    col(k, acc);
 #pragma unroll
-    for (int j = 1; j < 14; j++) T[k + j] += (uint64_t)m * c::P28[j];
+    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * c::P28[k - i];
+    m[k] = ((uint32_t)acc * c::PINV28) & M28;
+    acc += (uint64_t)m[k] * c::P28[0];
+    acc >>= 28;
   }
-  uint32_t t[14];
 #pragma unroll
   for (int k = 14; k < 27; k++) {
-    t[k - 14] = (uint32_t)T[k] & M28;
-    T[k + 1] += T[k] >> 28;
+    col(k, acc);
+#pragma unroll
+    for (int i = k - 13; i < 14; i++) acc += (uint64_t)m[i] * c::P28[k - i];
+    t[k - 14] = (uint32_t)acc & M28;
+    acc >>= 28;
   }
-  t[13] = (uint32_t)T[27];   // result < 2p < 2^382: fits
+  t[13] = (uint32_t)acc;   // result < 2p < 2^382: fits
   return fp_reduce_once(pack28(t));
 }
 
@@ -262,15 +256,10 @@ CESS_HD fp mul(const fp& a0, const fp& b0) {
   uint32_t x[14], y[14];
   unpack28(a, x);
   unpack28(b, y);
-  fp r = mont28([&](uint64_t (&T)[28]) {
+  fp r = mont28([&](int k, uint64_t& acc) {
 #pragma unroll
-    for (int k = 0; k < 27; k++) {
-      uint64_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < 14; i++)
-        if (k - i >= 0 && k - i < 14) acc += (uint64_t)x[i] * y[k - i];
-      T[k] = acc;
-    }
+    for (int i = 0; i < 14; i++)
+      if (k - i >= 0 && k - i < 14) acc += (uint64_t)x[i] * y[k - i];
   });
   seq(r);
   return r;
@@ -285,18 +274,13 @@ CESS_HD fp sqr(const fp& a0) {
   unpack28(a, x);
 #pragma unroll
   for (int i = 0; i < 14; i++) x2[i] = x[i] << 1;
-  fp r = mont28([&](uint64_t (&T)[28]) {
+  fp r = mont28([&](int k, uint64_t& acc) {
 #pragma unroll
-    for (int k = 0; k < 27; k++) {
-      uint64_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < 14; i++) {
-        const int j = k - i;
-        if (j > i && j < 14) acc += (uint64_t)x[i] * x2[j];
-      }
-      if ((k & 1) == 0 && (k >> 1) < 14) acc += (uint64_t)x[k >> 1] * x[k >> 1];
-      T[k] = acc;
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j > i && j < 14) acc += (uint64_t)x[i] * x2[j];
     }
+    if ((k & 1) == 0 && (k >> 1) < 14) acc += (uint64_t)x[k >> 1] * x[k >> 1];
   });
   seq(r);
   return r;

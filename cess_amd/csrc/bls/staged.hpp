@@ -277,10 +277,23 @@ CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& s
       case FE_LOAD: copy12(acc, slot(arg)); break;
       case FE_STORE: copy12(slot(arg), acc); break;
       case FE_MUL: mul12(acc, slot(arg)); break;
-      case FE_SQN:
+      case FE_SQN: {
+#if defined(CESS_FE_SQN_REGS)
+        // square run with the accumulator held in registers (one load/store per run)
+        fp12 t;
+        fp2* e = &t.c0.c0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) e[k] = acc.ld(k);
+#pragma unroll 1
+        for (int r = 0; r < arg; r++) t = cyclotomic_square(t);
+#pragma unroll
+        for (int k = 0; k < 6; k++) acc.st(k, e[k]);
+#else
 #pragma unroll 1
         for (int r = 0; r < arg; r++) cycsq12(acc);
+#endif
         break;
+      }
       case FE_CONJ: conj12(acc); break;
       case FE_FROB: frob12(acc, arg); break;
       case FE_INV: inv12(acc); break;

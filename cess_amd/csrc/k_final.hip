@@ -6,6 +6,7 @@
 // seven HBM slots (uint4 SoA, stride = context capacity) for the cold Fp12
 // temporaries; the Miller-loop output is slot SL_F.
 #include <hip/hip_runtime.h>
+#define CESS_FE_SQN_REGS 1
 #include "soa.hpp"
 
 using namespace bls;

@@ -15,6 +15,6 @@ echo "trace ok"
 timeout -k 10 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
   name=$(echo $grp | tr ' ' '_' | cut -c1-40)
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_final|k_miller" --output-format csv -d $OUT/pmc_$name -o run -- python3 bench.py --n $N --steps 1 --warmup 0 --cpu-sample 0 > $OUT/pmc_$name.log 2>&1 || { echo "pmc pass $grp failed"; tail -5 $OUT/pmc_$name.log; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_final|k_miller|k_prepare|k_hash|k_decode_sig|k_decode_pk" --output-format csv -d $OUT/pmc_$name -o run -- python3 bench.py --n $N --steps 1 --warmup 0 --cpu-sample 0 > $OUT/pmc_$name.log 2>&1 || { echo "pmc pass $grp failed"; tail -5 $OUT/pmc_$name.log; }
 done
 find $OUT -name "*.csv" | head -50

@@ -33,6 +33,12 @@ __global__ void k_rlc_pairs(uint32_t, const uint32_t*, const uint32_t*, uint64_t
                             uint32_t*, uint32_t*);
 __global__ void k_fp12_prod(uint32_t, const uint4*, uint64_t, uint4*);
 __global__ void k_gt_prod(uint32_t, const uint8_t*, uint4*, uint8_t*);
+__global__ void k_g1_sum_segs(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*, uint64_t, uint32_t*,
+                              uint64_t);
+__global__ void k_rlc_pairs_multi(uint32_t, uint32_t, const uint32_t*, const uint32_t*, const uint8_t*, uint8_t*,
+                                  uint8_t*, uint32_t*, uint32_t*);
+__global__ void k_rep_rows(uint32_t, uint32_t, uint32_t, const uint4*, uint4*);
+__global__ void k_fp12_prod_multi(uint32_t, uint32_t, const uint4*, uint4*);
 
 namespace {
 
@@ -74,6 +80,7 @@ struct RlcState {
   uint64_t checks = 0, leaves = 0, leaf_sigs = 0;
   DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
   DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, acc, slots, fin_code, fin_bm, gt, gts, tmp;
+  DevBuf seg, part2, rec_coeffs;
 };
 
 }  // namespace
@@ -429,53 +436,88 @@ extern "C" int cess_bls_stage_times(cess_bls_ctx* c, const char** names, double*
 // of kRlcLeaf records, which are verified per signature, so the final codes are
 // those of cess_bls_verify_batch (up to the 2^-127 soundness error).
 // ---------------------------------------------------------------------------
-static constexpr uint64_t kRlcLeaf = 2048;
+static constexpr uint64_t kRlcLeaf = 2048;   // records verified per signature
+static constexpr uint64_t kRlcFan = 16;     // bisection fan-out per level
 
-// out (stride out_stride) = sum of in[perm[off + j]], j < cnt  (two passes)
-static int rlc_sum(cess_bls_ctx* c, RlcState& R, hipStream_t s, uint64_t off, uint64_t cnt, const uint32_t* in,
-                   uint64_t in_stride, uint32_t* out, uint64_t out_stride) {
-  uint64_t B = std::min<uint64_t>(1024, std::max<uint64_t>(1, (cnt + 255) / 256));
-  if (R.part.ensure(B * 36 * 4)) return CESS_BLS_E_OOM;
-  hipLaunchKernelGGL(k_g1_sum, dim3((unsigned)B), dim3(256), 0, s, cnt, R.d_perm.as<uint32_t>(), off, in, in_stride,
-                     R.part.as<uint32_t>(), B);
-  hipLaunchKernelGGL(k_g1_sum, dim3(1), dim3(256), 0, s, B, (const uint32_t*)nullptr, (uint64_t)0,
-                     (const uint32_t*)R.part.as<uint32_t>(), B, out, out_stride);
+// Segmented sums: out[s] (stride out_stride) = sum of in[perm[off_s + j]], j < cnt_s.
+// Two passes of k_g1_sum_segs (B partial sums per segment, then one).
+static int rlc_sums(cess_bls_ctx* c, RlcState& R, hipStream_t s, const std::vector<uint64_t>& off,
+                    const std::vector<uint64_t>& cnt, const uint32_t* in, uint64_t in_stride, uint32_t* out,
+                    uint64_t out_stride) {
+  const uint64_t ns = off.size();
+  uint64_t mx = 1;
+  for (uint64_t v : cnt) mx = std::max(mx, v);
+  const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(1, 1024 / ns), (mx + 255) / 256));
+  std::vector<uint64_t> h(4 * ns);
+  for (uint64_t q = 0; q < ns; q++) h[q] = off[q], h[ns + q] = cnt[q], h[2 * ns + q] = q * B, h[3 * ns + q] = B;
+  if (R.seg.ensure(h.size() * 8) || R.part.ensure(ns * B * 36 * 4)) return CESS_BLS_E_OOM;
+  HIPCHK(hipMemcpyAsync(R.seg.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+  const uint64_t* d = R.seg.as<uint64_t>();
+  hipLaunchKernelGGL(k_g1_sum_segs, dim3((unsigned)B, (unsigned)ns), dim3(256), 0, s, d, d + ns,
+                     (const uint32_t*)R.d_perm.as<uint32_t>(), in, in_stride, R.part.as<uint32_t>(), ns * B);
+  hipLaunchKernelGGL(k_g1_sum_segs, dim3(1, (unsigned)ns), dim3(256), 0, s, d + 2 * ns, d + 3 * ns,
+                     (const uint32_t*)nullptr, (const uint32_t*)R.part.as<uint32_t>(), ns * B, out, out_stride);
   HIPCHK(hipGetLastError());
+  // the host vector h must outlive the async copy
+  HIPCHK(hipStreamSynchronize(s));
   return CESS_BLS_OK;
 }
 
-// one RLC check over perm positions [a, b): *ok = product of the K+1 pairings
-// is 1; gt_out (optional) receives the Gt value (576 canonical bytes)
-static int rlc_check(cess_bls_ctx* c, RlcState& R, uint64_t a, uint64_t b, bool* ok, uint8_t* gt_out) {
+// RLC checks of NR perm-position ranges in one batch: ok[r] = the product of
+// range r's K+1 pairings is 1.  gt_out (optional, NR == 1): its Gt value.
+static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
+                           std::vector<uint8_t>& ok, uint8_t* gt_out) {
   hipStream_t s = c->stream;
-  const uint32_t K = R.K;
-  R.checks++;
-  int r = rlc_sum(c, R, s, a, b - a, R.P.as<uint32_t>(), R.n, R.S.as<uint32_t>(), 1);
-  if (r) return r;
-  for (uint32_t g = 0; g < K; g++) {
-    uint64_t lo = std::max(a, R.gbeg[g]), hi = std::min(b, R.gbeg[g + 1]);
-    r = rlc_sum(c, R, s, lo, hi > lo ? hi - lo : 0, R.Q.as<uint32_t>(), R.n, R.Qs.as<uint32_t>() + g, K);
-    if (r) return r;
+  const uint32_t K = R.K, NR = (uint32_t)rg.size(), M = NR * K;
+  R.checks += NR;
+  std::vector<uint64_t> so(NR), sc(NR), qo(M), qc(M);
+  for (uint32_t r = 0; r < NR; r++) {
+    const uint64_t a = rg[r].first, b = rg[r].second;
+    so[r] = a, sc[r] = b - a;
+    for (uint32_t g = 0; g < K; g++) {
+      const uint64_t lo = std::max(a, R.gbeg[g]), hi = std::min(b, R.gbeg[g + 1]);
+      qo[r * K + g] = lo, qc[r * K + g] = hi > lo ? hi - lo : 0;
+    }
   }
-  hipLaunchKernelGGL(k_rlc_pairs, dim3((K + 63) / 64), dim3(64), 0, s, K, (const uint32_t*)R.S.as<uint32_t>(),
-                     (const uint32_t*)R.Qs.as<uint32_t>(), (uint64_t)K, (const uint8_t*)R.pk_usable.as<uint8_t>(),
+  int r = 0;
+  r |= R.S.ensure((uint64_t)NR * 36 * 4) | R.Qs.ensure((uint64_t)M * 36 * 4);
+  r |= R.rec_code.ensure(M) | R.rec_inf.ensure(M) | R.rec_sig.ensure((uint64_t)M * CESS_W_G1 * 4);
+  r |= R.rec_h.ensure((uint64_t)M * CESS_W_G1 * 4) | R.rec_f.ensure((uint64_t)M * CESS_W_FP12 * 4);
+  r |= R.acc.ensure((uint64_t)NR * CESS_W_FP12 * 4) | R.slots.ensure((uint64_t)NR * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
+  r |= R.fin_code.ensure(NR) | R.fin_bm.ensure(((NR + 63) / 64) * 8) | R.gt.ensure((uint64_t)NR * 576);
+  if (NR > 1) r |= R.rec_coeffs.ensure((uint64_t)M * CESS_W_COEFFS * 4);
+  if (r) return CESS_BLS_E_OOM;
+  r = rlc_sums(c, R, s, so, sc, R.P.as<uint32_t>(), R.n, R.S.as<uint32_t>(), NR);
+  if (r) return r;
+  r = rlc_sums(c, R, s, qo, qc, R.Q.as<uint32_t>(), R.n, R.Qs.as<uint32_t>(), M);
+  if (r) return r;
+  const uint4* coeffs = R.pk_coeffs.as<uint4>();
+  if (NR > 1) {
+    const uint64_t rows = CESS_W_COEFFS / 4, tot = rows * M;
+    hipLaunchKernelGGL(k_rep_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, (uint32_t)rows, NR, K,
+                       coeffs, R.rec_coeffs.as<uint4>());
+    coeffs = R.rec_coeffs.as<uint4>();
+  }
+  hipLaunchKernelGGL(k_rlc_pairs_multi, dim3((M + 63) / 64), dim3(64), 0, s, NR, K, (const uint32_t*)R.S.as<uint32_t>(),
+                     (const uint32_t*)R.Qs.as<uint32_t>(), (const uint8_t*)R.pk_usable.as<uint8_t>(),
                      R.rec_code.as<uint8_t>(), R.rec_inf.as<uint8_t>(), R.rec_sig.as<uint32_t>(), R.rec_h.as<uint32_t>());
-  hipLaunchKernelGGL(k_miller, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, s, (uint64_t)K,
+  hipLaunchKernelGGL(k_miller, dim3((M + kBlock - 1) / kBlock), dim3(kBlock), 0, s, (uint64_t)M,
                      (const uint8_t*)R.rec_code.as<uint8_t>(), (const uint8_t*)R.rec_inf.as<uint8_t>(),
                      (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
-                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)R.pk_coeffs.as<uint4>(), R.rec_f.as<uint4>(),
-                     (uint64_t)K);
-  hipLaunchKernelGGL(k_fp12_prod, dim3(1), dim3(64), 0, s, K, (const uint4*)R.rec_f.as<uint4>(), (uint64_t)K,
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), coeffs, R.rec_f.as<uint4>(), (uint64_t)M);
+  hipLaunchKernelGGL(k_fp12_prod_multi, dim3((NR + 63) / 64), dim3(64), 0, s, NR, K, (const uint4*)R.rec_f.as<uint4>(),
                      R.acc.as<uint4>());
-  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, 1, s));
-  hipLaunchKernelGGL(k_final, dim3(1), dim3(kBlock), 0, s, (uint64_t)1, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
-                     R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(), R.gt.as<uint8_t>(), (uint64_t)1);
+  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
+  hipLaunchKernelGGL(k_final, dim3((NR + kBlock - 1) / kBlock), dim3(kBlock), 0, s, (uint64_t)NR,
+                     R.fin_code.as<uint8_t>(), R.acc.as<uint4>(), R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(),
+                     gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, (uint64_t)NR);
   HIPCHK(hipGetLastError());
-  uint8_t code = 0xff;
-  HIPCHK(hipMemcpyAsync(&code, R.fin_code.p, 1, hipMemcpyDeviceToHost, s));
+  ok.assign(NR, 0);
+  std::vector<uint8_t> codes(NR);
+  HIPCHK(hipMemcpyAsync(codes.data(), R.fin_code.p, NR, hipMemcpyDeviceToHost, s));
   if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  *ok = code == CODE_OK;
+  for (uint32_t q = 0; q < NR; q++) ok[q] = codes[q] == CODE_OK;
   return CESS_BLS_OK;
 }
 
@@ -552,13 +594,9 @@ extern "C" int cess_bls_rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs
   // 2. device buffers
   int r = 0;
   r |= R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4) | R.d_perm.ensure(n * 4) | R.d_seed.ensure(32);
-  r |= R.S.ensure(36 * 4) | R.Qs.ensure((uint64_t)K * 36 * 4) | R.pk_in.ensure((uint64_t)K * 96);
+  r |= R.pk_in.ensure((uint64_t)K * 96);
   r |= R.pk_code.ensure(K) | R.pk_inf.ensure(K) | R.pk_aff.ensure((uint64_t)K * CESS_W_G2 * 4);
   r |= R.pk_coeffs.ensure((uint64_t)K * CESS_W_COEFFS * 4) | R.pk_usable.ensure(K);
-  r |= R.rec_code.ensure(K) | R.rec_inf.ensure(K) | R.rec_sig.ensure((uint64_t)K * CESS_W_G1 * 4);
-  r |= R.rec_h.ensure((uint64_t)K * CESS_W_G1 * 4) | R.rec_f.ensure((uint64_t)K * CESS_W_FP12 * 4);
-  r |= R.acc.ensure(CESS_W_FP12 * 4) | R.slots.ensure(CESS_W_FP12 * 4 * CESS_FE_SLOTS) | R.fin_code.ensure(1);
-  r |= R.fin_bm.ensure(8) | R.gt.ensure(576);
   if (r) return CESS_BLS_E_OOM;
   {
     uint32_t sw[8];
@@ -630,10 +668,10 @@ extern "C" int cess_bls_rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs
     HIPCHK(hipStreamSynchronize(s));   // hc/hi are reused by the next chunk
   }
   // 5. the batch check (this shard's Gt partial)
-  bool ok = false;
-  r = rlc_check(c, R, 0, n, &ok, gt_out);
+  std::vector<uint8_t> ok;
+  r = rlc_check_multi(c, R, {{0, n}}, ok, gt_out);
   if (r) return r;
-  R.local_ok = ok;
+  R.local_ok = ok[0] != 0;
   return CESS_BLS_OK;
 }
 
@@ -666,61 +704,56 @@ extern "C" int cess_bls_rlc_finish(cess_bls_ctx* c, int global_ok, uint8_t* code
   const uint64_t n = R.n;
   std::vector<uint8_t>& codes = R.codes;
   if (!global_ok && !R.local_ok) {
-    // bisection over perm positions; `known` = this range is known to fail
-    struct Rg {
-      uint64_t a, b;
-      bool known;
-    };
-    std::vector<Rg> work = {{0, n, true}};
-    std::vector<uint8_t> ls, lp, lm, lc;
-    std::vector<uint64_t> lo, li;
-    while (!work.empty()) {
-      Rg w = work.back();
-      work.pop_back();
-      if (w.b - w.a <= kRlcLeaf) {
-        // leaf: per-signature verification of the candidates (exact codes)
-        li.clear();
-        for (uint64_t j = w.a; j < w.b; j++)
-          if (codes[R.perm[j]] == 0) li.push_back(R.perm[j]);
-        if (li.empty()) continue;
-        const uint64_t m = li.size();
-        ls.resize(m * 48);
-        lp.resize(m * 96);
-        lm.clear();
-        lo.assign(1, 0);
-        for (uint64_t q = 0; q < m; q++) {
-          const uint64_t i = li[q];
-          memcpy(&ls[48 * q], R.sigs + 48 * i, 48);
-          memcpy(&lp[96 * q], R.pks + 96 * i, 96);
-          lm.insert(lm.end(), R.msgs + R.offs[i], R.msgs + R.offs[i + 1]);
-          lo.push_back(lm.size());
+    // batched bisection over perm positions: every failing range is split
+    // into up to kRlcFan parts, all parts of a level are checked in one batch;
+    // ranges of <= kRlcLeaf records are verified per signature (exact codes)
+    std::vector<std::pair<uint64_t, uint64_t>> level = {{0, n}}, parts, leaves;
+    std::vector<uint8_t> ok;
+    while (!level.empty()) {
+      parts.clear();
+      for (auto& w : level) {
+        const uint64_t len = w.second - w.first;
+        if (len <= kRlcLeaf) {
+          leaves.push_back(w);
+          continue;
         }
-        lc.resize(m);
-        int r = verify_host(c, m, ls.data(), lp.data(), lm.empty() ? nullptr : lm.data(), lo.data(), nullptr,
-                            lc.data(), nullptr, nullptr);
-        if (r) return r;
-        for (uint64_t q = 0; q < m; q++) codes[li[q]] = lc[q];
-        R.leaves++;
-        R.leaf_sigs += m;
-        continue;
+        const uint64_t fan = std::min<uint64_t>(kRlcFan, (len + kRlcLeaf - 1) / kRlcLeaf);
+        for (uint64_t q = 0; q < fan; q++)
+          parts.push_back({w.first + len * q / fan, w.first + len * (q + 1) / fan});
       }
-      bool ok = false;
-      if (!w.known) {
-        int r = rlc_check(c, R, w.a, w.b, &ok, nullptr);
+      level.clear();
+      if (!parts.empty()) {
+        int r = rlc_check_multi(c, R, parts, ok, nullptr);
         if (r) return r;
-        if (ok) continue;
+        for (size_t q = 0; q < parts.size(); q++)
+          if (!ok[q]) level.push_back(parts[q]);
       }
-      const uint64_t mid = w.a + (w.b - w.a) / 2;
-      // check the left half first; if it passes, the right half must fail
-      bool left_ok = false;
-      if (mid - w.a > kRlcLeaf) {
-        int r = rlc_check(c, R, w.a, mid, &left_ok, nullptr);
-        if (r) return r;
-        if (!left_ok) work.push_back({w.a, mid, true});
-      } else {
-        work.push_back({w.a, mid, true});
+    }
+    // leaves: one per-signature batch over all their candidate records
+    std::vector<uint64_t> li, lo = {0};
+    std::vector<uint8_t> ls, lp, lm, lc;
+    for (auto& w : leaves) {
+      for (uint64_t j = w.first; j < w.second; j++)
+        if (codes[R.perm[j]] == 0) li.push_back(R.perm[j]);
+      R.leaves++;
+    }
+    const uint64_t m = li.size();
+    if (m) {
+      ls.resize(m * 48);
+      lp.resize(m * 96);
+      for (uint64_t q = 0; q < m; q++) {
+        const uint64_t i = li[q];
+        memcpy(&ls[48 * q], R.sigs + 48 * i, 48);
+        memcpy(&lp[96 * q], R.pks + 96 * i, 96);
+        lm.insert(lm.end(), R.msgs + R.offs[i], R.msgs + R.offs[i + 1]);
+        lo.push_back(lm.size());
       }
-      work.push_back({mid, w.b, left_ok});
+      lc.resize(m);
+      int r = verify_host(c, m, ls.data(), lp.data(), lm.empty() ? nullptr : lm.data(), lo.data(), nullptr, lc.data(),
+                          nullptr, nullptr);
+      if (r) return r;
+      for (uint64_t q = 0; q < m; q++) codes[li[q]] = lc[q];
+      R.leaf_sigs += m;
     }
   }
   if (codes_out) memcpy(codes_out, codes.data(), n);

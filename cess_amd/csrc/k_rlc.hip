@@ -118,6 +118,92 @@ __global__ __launch_bounds__(256, 1) void k_g1_sum(uint64_t cnt, const uint32_t*
   if (t == 0) st_g1p(out, out_stride, blockIdx.x, acc);
 }
 
+// Segmented form (batched bisection): segment s = perm positions
+// [seg_off[s], seg_off[s] + seg_cnt[s]); grid (B, nseg); block (bx, s) writes
+// out[s * B + bx] (SoA stride out_stride).  With perm = nullptr the positions
+// index `in` directly (second pass over the partial sums).
+__global__ __launch_bounds__(256, 1) void k_g1_sum_segs(const uint64_t* __restrict__ seg_off,
+                                                        const uint64_t* __restrict__ seg_cnt,
+                                                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ in,
+                                                        uint64_t in_stride, uint32_t* __restrict__ out,
+                                                        uint64_t out_stride) {
+  __shared__ uint32_t L[36][256];
+  const uint32_t t = threadIdx.x, sg = blockIdx.y;
+  const uint64_t T = (uint64_t)gridDim.x * blockDim.x, off = seg_off[sg], cnt = seg_cnt[sg];
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + t; j < cnt; j += T) {
+    const uint64_t idx = perm ? perm[off + j] : off + j;
+    acc = proj_add(acc, ld_g1p(in, in_stride, (uint32_t)idx));
+  }
+#pragma unroll 1
+  for (uint32_t s = 128; s >= 1; s >>= 1) {
+    if (t >= s && t < 2 * s) {
+      const fp* e = &acc.x;
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+#pragma unroll
+        for (int l = 0; l < 12; l++) L[12 * w + l][t - s] = e[w].v[l];
+    }
+    __syncthreads();
+    if (t < s) {
+      g1p o;
+      fp* e = &o.x;
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+#pragma unroll
+        for (int l = 0; l < 12; l++) e[w].v[l] = L[12 * w + l][t];
+      acc = proj_add(acc, o);
+    }
+    __syncthreads();
+  }
+  if (t == 0) st_g1p(out, out_stride, sg * gridDim.x + blockIdx.x, acc);
+}
+
+// Batched check records: record j = r*K + g of range r (R ranges): pair 0 =
+// (S_r, -G2) on g == 0 only, pair 1 = (Q_{r,g}, pk_g).  Sums: S (stride R, r),
+// Qs (stride R*K, j).  Output in k_miller's SoA format (stride R*K).
+__global__ void k_rlc_pairs_multi(uint32_t R, uint32_t K, const uint32_t* __restrict__ S,
+                                  const uint32_t* __restrict__ Qs, const uint8_t* __restrict__ pk_usable,
+                                  uint8_t* __restrict__ code, uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff,
+                                  uint32_t* __restrict__ h_aff) {
+  const uint32_t m = R * K, j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t r = j / K, g = j % K;
+  uint8_t f = 0;
+  g1a s = {fp_zero(), fp_one(), true};
+  if (g == 0) s = proj_to_affine(ld_g1p(S, R, r));
+  if (s.inf) f |= INF_SIG;
+  g1a h = proj_to_affine(ld_g1p(Qs, m, j));
+  if (h.inf || !pk_usable[g]) f |= INF_PK;
+  st_fp(sig_aff, m, j, s.x);
+  st_fp(sig_aff + 12 * m, m, j, s.y);
+  st_fp(h_aff, m, j, h.x);
+  st_fp(h_aff + 12 * m, m, j, h.y);
+  inf[j] = f;
+  code[j] = 0;
+}
+
+// dst (stride R*K) record j <- src (stride K) record j % K, for every uint4 row
+__global__ void k_rep_rows(uint32_t rows, uint32_t R, uint32_t K, const uint4* __restrict__ src,
+                           uint4* __restrict__ dst) {
+  const uint64_t m = (uint64_t)R * K, w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= m * rows) return;
+  const uint64_t row = w / m, j = w % m;
+  dst[row * m + j] = src[row * K + j % K];
+}
+
+// acc slot r (stride R) = prod_{g < K} fin[r*K + g] (fin stride R*K); one lane per range
+__global__ void k_fp12_prod_multi(uint32_t R, uint32_t K, const uint4* __restrict__ fin, uint4* __restrict__ acc) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint64_t m = (uint64_t)R * K;
+  GlobF12 a{acc, R, r};
+  copy12(a, GlobF12{const_cast<uint4*>(fin), m, r * K});
+#pragma unroll 1
+  for (uint32_t g = 1; g < K; g++) mul12(a, GlobF12{const_cast<uint4*>(fin), m, r * K + g});
+}
+
 // Records j < m of the K+1-pair check: pair 0 carries S (record 0 only),
 // pair 1 carries (Q_j, pk_j).  pk_usable[j] = 0 for keys that are the identity
 // (their pairing term is 1).  Output in k_miller's SoA input format (stride m).

@@ -141,6 +141,18 @@ CESS_HD fp sub(const fp& a, const fp& b) {
   return r;
 }
 
+// Unreduced sum (no conditional subtraction): a + b < 2^384 for a, b < 2^383.
+// ONLY for values consumed by mul(): the Montgomery product accepts inputs up to
+// 8p (a*b < 64 p^2 < p R, R = 2^392) and returns a fully reduced value.  Never
+// feed an unreduced value to sub/neg/sqr/eq or store it.
+CESS_HD fp add_nr(const fp& a, const fp& b) {
+  fp t;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) t.v[i] = addc32(a.v[i], b.v[i], carry, &carry);
+  return t;
+}
+
 CESS_HD fp dbl(const fp& a) { return add(a, a); }
 
 CESS_HD bool is_zero(const fp& a) {
@@ -370,8 +382,57 @@ CESS_HD void raw_to_be48(const fp& a, uint8_t* b) {
 // ---------------------------------------------------------------------------
 CESS_HD fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
 CESS_HD fp2 fp2_one() { return {fp_one(), fp_zero()}; }
-CESS_HD fp2 add(const fp2& a, const fp2& b) { return {add(a.c0, b.c0), add(a.c1, b.c1)}; }
-CESS_HD fp2 sub(const fp2& a, const fp2& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1)}; }
+// Fp2 add/sub with the two components' carry chains interleaved limb by limb
+// (one chain alone stalls on the VCC carry hazard between dependent links).
+CESS_HD fp2 add(const fp2& a, const fp2& b) {
+  fp t0, t1, s0, s1;
+  uint32_t c0 = 0, c1 = 0, b0 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    t0.v[i] = addc32(a.c0.v[i], b.c0.v[i], c0, &c0);
+    t1.v[i] = addc32(a.c1.v[i], b.c1.v[i], c1, &c1);
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    s0.v[i] = subc32(t0.v[i], c::P_RAW[i], b0, &b0);
+    s1.v[i] = subc32(t1.v[i], c::P_RAW[i], b1, &b1);
+  }
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.v[i] = b0 ? t0.v[i] : s0.v[i];
+    r.c1.v[i] = b1 ? t1.v[i] : s1.v[i];
+  }
+  return r;
+}
+CESS_HD fp2 sub(const fp2& a, const fp2& b) {
+  fp t0, t1;
+  uint32_t b0 = 0, b1 = 0, c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    t0.v[i] = subc32(a.c0.v[i], b.c0.v[i], b0, &b0);
+    t1.v[i] = subc32(a.c1.v[i], b.c1.v[i], b1, &b1);
+  }
+  const uint32_t m0 = 0u - b0, m1 = 0u - b1;
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.v[i] = addc32(t0.v[i], c::P_RAW[i] & m0, c0, &c0);
+    r.c1.v[i] = addc32(t1.v[i], c::P_RAW[i] & m1, c1, &c1);
+  }
+  return r;
+}
+// unreduced, for mul() operands only (see add_nr(fp, fp))
+CESS_HD fp2 add_nr(const fp2& a, const fp2& b) {
+  fp2 r;
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.v[i] = addc32(a.c0.v[i], b.c0.v[i], c0, &c0);
+    r.c1.v[i] = addc32(a.c1.v[i], b.c1.v[i], c1, &c1);
+  }
+  return r;
+}
 CESS_HD fp2 dbl(const fp2& a) { return {dbl(a.c0), dbl(a.c1)}; }
 CESS_HD fp2 neg(const fp2& a) { return {neg(a.c0), neg(a.c1)}; }
 CESS_HD fp2 conj(const fp2& a) { return {a.c0, neg(a.c1)}; }
@@ -382,10 +443,12 @@ CESS_HD fp2 mul3(const fp2& a) { return {mul3(a.c0), mul3(a.c1)}; }
 CESS_HD fp2 mul4(const fp2& a) { return {mul4(a.c0), mul4(a.c1)}; }
 CESS_HD fp2 mul8(const fp2& a) { return {mul8(a.c0), mul8(a.c1)}; }
 
+// Inputs may be unreduced (each component < 4p, from add_nr): only mul() and
+// add_nr() touch them, and every output is reduced.
 CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   fp t0 = mul(a.c0, b.c0);
   fp t1 = mul(a.c1, b.c1);
-  fp t2 = mul(add(a.c0, a.c1), add(b.c0, b.c1));
+  fp t2 = mul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1));
   return {sub(t0, t1), sub(sub(t2, t0), t1)};
 }
 CESS_HD fp2 sqr(const fp2& a) {
@@ -450,14 +513,17 @@ CESS_HD fp6 dbl(const fp6& a) { return {dbl(a.c0), dbl(a.c1), dbl(a.c2)}; }
 CESS_HD bool eq(const fp6& a, const fp6& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1) && eq(a.c2, b.c2); }
 // * v
 CESS_HD fp6 mul_v(const fp6& a) { return {mul_nr(a.c2), a.c0, a.c1}; }
+// unreduced, for mul() operands only
+CESS_HD fp6 add_nr(const fp6& a, const fp6& b) { return {add_nr(a.c0, b.c0), add_nr(a.c1, b.c1), add_nr(a.c2, b.c2)}; }
 
 CESS_HD fp6 mul(const fp6& a, const fp6& b) {
   fp2 t0 = mul(a.c0, b.c0);
   fp2 t1 = mul(a.c1, b.c1);
   fp2 t2 = mul(a.c2, b.c2);
-  fp2 c0 = add(mul_nr(sub(sub(mul(add(a.c1, a.c2), add(b.c1, b.c2)), t1), t2)), t0);
-  fp2 c1 = add(sub(sub(mul(add(a.c0, a.c1), add(b.c0, b.c1)), t0), t1), mul_nr(t2));
-  fp2 c2 = add(sub(sub(mul(add(a.c0, a.c2), add(b.c0, b.c2)), t0), t2), t1);
+  // inputs may be unreduced (< 2p per Fp component); sums feed mul() only
+  fp2 c0 = add(mul_nr(sub(sub(mul(add_nr(a.c1, a.c2), add_nr(b.c1, b.c2)), t1), t2)), t0);
+  fp2 c1 = add(sub(sub(mul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1)), t0), t1), mul_nr(t2));
+  fp2 c2 = add(sub(sub(mul(add_nr(a.c0, a.c2), add_nr(b.c0, b.c2)), t0), t2), t1);
   return {c0, c1, c2};
 }
 CESS_HD fp6 sqr(const fp6& a) {
@@ -479,7 +545,7 @@ CESS_HD fp6 mul_by_01(const fp6& a, const fp2& b0, const fp2& b1) {
   fp2 t0 = mul(a.c0, b0);
   fp2 t1 = mul(a.c1, b1);
   fp2 c0 = add(mul_nr(mul(a.c2, b1)), t0);
-  fp2 c1 = sub(sub(mul(add(a.c0, a.c1), add(b0, b1)), t0), t1);
+  fp2 c1 = sub(sub(mul(add_nr(a.c0, a.c1), add_nr(b0, b1)), t0), t1);
   fp2 c2 = add(mul(a.c2, b0), t1);
   return {c0, c1, c2};
 }

@@ -140,7 +140,7 @@ CESS_HD void sqr12(const S& f) {
   fp6 x;
   {
     fp6 a0 = ld6(f, 0), a1 = ld6(f, 1);
-    x = mul(add(a0, a1), add(a0, mul_v(a1)));
+    x = mul(add_nr(a0, a1), add_nr(a0, mul_v(a1)));
   }
   st6(f, 0, sub(sub(x, ab), mul_v(ab)));
   st6(f, 1, dbl(ab));
@@ -160,7 +160,7 @@ CESS_HD void mul014(const S& f, const fp2& c0, const fp2& c1, const fp2& c4) {
   st6(f, 0, add(mul_v(bb), aa));
   fp6 u = add(aa, bb);
   CESS_MEMBAR();
-  fp6 t = mul_by_01(ld6(f, 1), c0, add(c1, c4));
+  fp6 t = mul_by_01(ld6(f, 1), c0, add_nr(c1, c4));
   st6(f, 1, sub(t, u));
 }
 
@@ -172,7 +172,7 @@ CESS_HD void mul12(const S& f, const G& g) {
   CESS_MEMBAR();
   t1 = mul(ld6(f, 1), ld6(g, 1));
   CESS_MEMBAR();
-  fp6 x = mul(add(ld6(f, 0), ld6(f, 1)), add(ld6(g, 0), ld6(g, 1)));
+  fp6 x = mul(add_nr(ld6(f, 0), ld6(f, 1)), add_nr(ld6(g, 0), ld6(g, 1)));
   st6(f, 1, sub(sub(x, t0), t1));
   st6(f, 0, add(t0, mul_v(t1)));
 }

@@ -451,8 +451,8 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   fp t2 = mul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1));
   return {sub(t0, t1), sub(sub(t2, t0), t1)};
 }
-CESS_HD fp2 sqr(const fp2& a) {
-  fp t0 = mul(add(a.c0, a.c1), sub(a.c0, a.c1));
+CESS_HD fp2 sqr(const fp2& a) {   // a must be reduced (sub below)
+  fp t0 = mul(add_nr(a.c0, a.c1), sub(a.c0, a.c1));
   fp t1 = mul(a.c0, a.c1);
   return {t0, dbl(t1)};
 }

@@ -1,0 +1,111 @@
+"""GPU: edge cases of the batch boundary -- partial bitmap words, empty
+batches, the device-resident entry point against the host one, the adversarial
+mix of BASELINE config[4] at moderate size (codes exact against the oracle's
+fixture codes), and identity keys in RLC mode."""
+import json
+import os
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _signed(ctx, n, seed, msg_len=32):
+    rng = random.Random(seed)
+    sks = [rng.randrange(1, R).to_bytes(32, "big") for _ in range(n)]
+    msgs = [rng.randbytes(msg_len) for _ in range(n)]
+    return ctx.sign(sks, msgs), msgs, ctx.public_keys(sks)
+
+
+def _offs(msgs):
+    o = [0]
+    for m in msgs:
+        o.append(o[-1] + len(m))
+    return o
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 130])
+def test_partial_bitmap_words(ctx, n):
+    sigs, msgs, pks = _signed(ctx, n, n)
+    msgs[-1] = bytes(len(msgs[-1]))           # last record forged
+    codes, words = ctx.verify_fixed(b"".join(sigs), b"".join(pks), b"".join(msgs), _offs(msgs))
+    assert list(codes) == [0] * (n - 1) + [5]
+    assert len(words) == (n + 63) // 64
+    bits = [(words[i >> 6] >> (i & 63)) & 1 for i in range(n)]
+    assert bits == [1] * (n - 1) + [0]
+    if n % 64:
+        assert words[-1] >> (n % 64) == 0      # no bits set past the last record
+
+
+def test_empty_batch(ctx):
+    assert ctx.verify_codes([]) == b""
+    codes, words = ctx.verify_fixed(b"", b"", b"", [0])
+    assert codes == b"" and words == []
+
+
+def test_device_entry_matches_host(ctx):
+    import torch
+    n = 256
+    sigs, msgs, pks = _signed(ctx, n, 11)
+    msgs[7] = bytes(32)
+    S, P, M = b"".join(sigs), b"".join(pks), b"".join(msgs)
+    expect, ewords = ctx.verify_fixed(S, P, M, _offs(msgs))
+    dev = torch.device("cuda", 0)
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_s, d_p, d_m = t(S), t(P), t(M)
+    d_o = torch.tensor(_offs(msgs), dtype=torch.int64, device=dev)
+    d_c = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_b = torch.zeros(n // 64, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ctx.verify_device(n, d_s.data_ptr(), d_p.data_ptr(), d_m.data_ptr(), d_o.data_ptr(), d_c.data_ptr(),
+                      d_b.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert bytes(d_c.cpu().tolist()) == expect
+    assert [w & ((1 << 64) - 1) for w in d_b.cpu().tolist()] == ewords
+
+
+def test_adversarial_mix_exact_codes(ctx, vectors):
+    """config[4] shape at 20,000 records: 1 % forged, 1 % adversarial fixture
+    records (non-subgroup, off-curve, x >= p, flag errors, identities) through
+    both the fixed-stride and the variable-length entry points."""
+    n = 20000
+    sigs, msgs, pks = _signed(ctx, n, 12)
+    rng = random.Random(13)
+    expect = [0] * n
+    cases = [c for c in vectors["cases"] if len(c["sig"]) == 96 and len(c["pk"]) == 192]
+    idx = rng.sample(range(n), 400)
+    for i in idx[:200]:
+        msgs[i] = rng.randbytes(32)
+        expect[i] = 5
+    for j, i in enumerate(idx[200:]):
+        c = cases[j % len(cases)]
+        sigs[i], msgs[i], pks[i] = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+        expect[i] = c["code"]
+    codes, _ = ctx.verify_fixed(b"".join(sigs), b"".join(pks), b"".join(msgs), _offs(msgs))
+    assert list(codes) == expect
+    # variable-length path, with the golden wrong-length records appended
+    lc = vectors["length_cases"]
+    recs = list(zip(sigs, msgs, pks)) + [(bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"]))
+                                         for c in lc]
+    assert list(ctx.verify_codes(recs)) == expect + [c["code"] for c in lc]
+
+
+def test_rlc_identity_keys(ctx, vectors):
+    """RLC groups by key encoding: the identity key (its pairing term is 1) and
+    the (O, O) pair must come out exactly as in the per-signature path."""
+    sigs, msgs, pks = _signed(ctx, 3000, 14)
+    ident = next(c for c in vectors["cases"] if c["sig"].startswith("c0") and c["pk"].startswith("c0"))
+    O_sig, O_pk = bytes.fromhex(ident["sig"]), bytes.fromhex(ident["pk"])
+    for i in (5, 700, 2999):
+        sigs[i], pks[i] = O_sig, O_pk                 # (O, O): accepted for any message
+    pks[1000] = O_pk                                  # valid sig, identity key: rejected
+    S, P, M, o = b"".join(sigs), b"".join(pks), b"".join(msgs), _offs(msgs)
+    expect, _ = ctx.verify_fixed(S, P, M, o)
+    codes, _, st = ctx.verify_rlc(S, P, M, o, seed=bytes(range(32)))
+    assert codes == expect
+    assert expect[5] == expect[700] == 0 and expect[1000] == 5
+    assert json.dumps(st)

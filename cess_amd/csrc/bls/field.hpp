@@ -486,18 +486,20 @@ CESS_HD bool sqrt(fp2& r, const fp2& a) {
   fp n = add(sqr(a.c0), sqr(a.c1));
   fp s;
   if (!sqrt(s, n)) return false;
-  // exactly one of (a0 + s)/2, (a0 - s)/2 is a nonzero square (a1 != 0)
+  // exactly one of al = (a0 + s)/2, al' = (a0 - s)/2 is a nonzero square
+  // (a1 != 0), and al * al' = -a1^2/4.  With t = al^((p-3)/4):
+  //   al square:     x = (t al, a1 t / 2)
+  //   al non-square: t^2 al = -1, so sqrt(al') = -a1 t / 2 and a1 / (2 sqrt(al'))
+  //                  = -1/t = t al:  x = (-a1 t / 2, t al)
+  // (p = 3 mod 8).  One exponentiation instead of a second one on al'; the
+  // final check below covers both branches.
   const fp half = fp_from(c::HALF);
-  fp al = mul(add(a.c0, s), half);
-  fp t = pow_fixed(al, c::EXP_SQRT_RATIO);  // al^((p-3)/4)
-  if (!eq(mul(sqr(t), al), fp_one())) {
-    al = mul(sub(a.c0, s), half);
-    t = pow_fixed(al, c::EXP_SQRT_RATIO);
-  }
-  // x0 = sqrt(al) = t * al ; 1/x0 = t ; x1 = a1 / (2 x0) = a1 * t * half
-  fp x0 = mul(t, al);
-  fp x1 = mul(mul(a.c1, t), half);
-  r = {x0, x1};
+  const fp al = mul(add(a.c0, s), half);
+  const fp t = pow_fixed(al, c::EXP_SQRT_RATIO);  // al^((p-3)/4)
+  const fp u = mul(t, al);                        // sqrt(al) if al is a square
+  const fp w = mul(mul(a.c1, t), half);           // a1 t / 2
+  const bool sq = eq(mul(u, t), fp_one());        // t^2 al == 1
+  r = {select(sq, u, neg(w)), select(sq, w, u)};
   return eq(sqr(r), a);
 }
 

@@ -56,3 +56,27 @@ def test_staged_matches_valuebased(emu, vectors):
         assert c1 == c2 == c["code"], c["name"]
         if c1 in (0, 5):
             assert bytes(g1) == bytes(g2), c["name"]
+
+
+def test_fp2_sqrt_against_oracle(emu):
+    """The single-exponentiation Fp2 square root (field.hpp sqrt(fp2)) agrees
+    with the oracle's square test on random squares and non-squares, including
+    a0 + s non-square branches and real (a1 = 0) inputs."""
+    import random
+
+    import oracle.bls_oracle as o
+    rng = random.Random(99)
+    limbs = lambda v: (ctypes.c_uint32 * 12)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+    val = lambda arr: sum(arr[i] << (32 * i) for i in range(12))
+    seen = {True: 0, False: 0}
+    cases = [(rng.randrange(o.P), rng.randrange(o.P)) for _ in range(60)]
+    cases += [o.f2_sqr((rng.randrange(o.P), rng.randrange(o.P))) for _ in range(60)]
+    cases += [(rng.randrange(o.P), 0) for _ in range(10)]
+    for a in cases:
+        r0, r1 = (ctypes.c_uint32 * 12)(), (ctypes.c_uint32 * 12)()
+        ok = bool(emu.emu_fp2_sqrt(limbs(a[0]), limbs(a[1]), r0, r1))
+        assert ok == o.f2_is_square(a), a
+        if ok:
+            assert o.f2_sqr((val(r0), val(r1))) == tuple(x % o.P for x in a)
+        seen[ok] += 1
+    assert seen[True] > 50 and seen[False] > 20

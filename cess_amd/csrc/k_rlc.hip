@@ -50,6 +50,31 @@ __device__ void rlc_scalar(const uint32_t* seed, uint64_t i, uint32_t (&k)[4]) {
 
 }  // namespace
 
+// [k]P for a 128-bit k and affine P (not the identity): 2-bit fixed windows with
+// the table {P, 2P, 3P}; the window digit differs per lane, so the addition is
+// computed every window and kept by a select (no divergent branches): 128
+// doublings + 64 complete additions (a per-bit ladder costs 128 + 128 here,
+// since some lane of the wave always takes the add).
+__device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint32_t (&k)[4]) {
+  const g1p T1 = {px, py, fp_one()};
+  const g1p T2 = proj_dbl(T1);
+  const g1p T3 = proj_add_mixed(T2, px, py);
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (int w = 3; w >= 0; w--) {
+#pragma unroll 1
+    for (int b = 30; b >= 0; b -= 2) {
+      acc = proj_dbl(proj_dbl(acc));
+      const uint32_t d = (k[w] >> b) & 3u;
+      const g1p t = {select(d == 1, T1.x, select(d == 2, T2.x, T3.x)), select(d == 1, T1.y, select(d == 2, T2.y, T3.y)),
+                     select(d == 1, T1.z, select(d == 2, T2.z, T3.z))};
+      const g1p sum = proj_add(acc, t);
+      acc = {select(d != 0, sum.x, acc.x), select(d != 0, sum.y, acc.y), select(d != 0, sum.z, acc.z)};
+    }
+  }
+  return acc;
+}
+
 __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
                                     const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
                                     const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
@@ -61,21 +86,8 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   if (code[i] == 0) {
     uint32_t k[4];
     rlc_scalar(seed, index_base + i, k);
-    const bool use_s = (fl & INF_SIG) == 0, use_h = (fl & INF_PK) == 0;
-    fp sx = ld_fp(sig_aff, stride, i), sy = ld_fp(sig_aff + 12 * stride, stride, i);
-    fp hx = ld_fp(h_aff, stride, i), hy = ld_fp(h_aff + 12 * stride, stride, i);
-#pragma unroll 1
-    for (int w = 3; w >= 0; w--) {
-#pragma unroll 1
-      for (int b = 31; b >= 0; b--) {
-        if (use_s) p = proj_dbl(p);
-        if (use_h) q = proj_dbl(q);
-        if ((k[w] >> b) & 1u) {
-          if (use_s) p = proj_add_mixed(p, sx, sy);
-          if (use_h) q = proj_add_mixed(q, hx, hy);
-        }
-      }
-    }
+    if ((fl & INF_SIG) == 0) p = mul128_w2(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), k);
+    if ((fl & INF_PK) == 0) q = mul128_w2(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), k);
   }
   st_g1p(P, out_stride, i, p);
   st_g1p(Q, out_stride, i, q);

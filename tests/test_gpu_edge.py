@@ -47,25 +47,54 @@ def test_empty_batch(ctx):
     assert codes == b"" and words == []
 
 
+def _hip():
+    """The HIP runtime libcess_bls.so itself links (/opt/rocm), via ctypes, so
+    device buffers come from the same runtime instance as the kernels (torch
+    bundles a second HIP runtime; initialising both in one process is
+    order-sensitive)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    hip.hipDeviceSynchronize.argtypes = []
+    return hip
+
+
 def test_device_entry_matches_host(ctx):
-    import torch
+    import ctypes
+    hip = _hip()
     n = 256
     sigs, msgs, pks = _signed(ctx, n, 11)
     msgs[7] = bytes(32)
     S, P, M = b"".join(sigs), b"".join(pks), b"".join(msgs)
     expect, ewords = ctx.verify_fixed(S, P, M, _offs(msgs))
-    dev = torch.device("cuda", 0)
-    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
-    d_s, d_p, d_m = t(S), t(P), t(M)
-    d_o = torch.tensor(_offs(msgs), dtype=torch.int64, device=dev)
-    d_c = torch.empty(n, dtype=torch.uint8, device=dev)
-    d_b = torch.zeros(n // 64, dtype=torch.int64, device=dev)
-    s = torch.cuda.current_stream(dev)
-    ctx.verify_device(n, d_s.data_ptr(), d_p.data_ptr(), d_m.data_ptr(), d_o.data_ptr(), d_c.data_ptr(),
-                      d_b.data_ptr(), s.cuda_stream)
-    torch.cuda.synchronize()
-    assert bytes(d_c.cpu().tolist()) == expect
-    assert [w & ((1 << 64) - 1) for w in d_b.cpu().tolist()] == ewords
+    offs = (ctypes.c_uint64 * (n + 1))(*_offs(msgs))
+    ptrs = []
+
+    def dev(data, size):
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), size) == 0
+        if data is not None:
+            assert hip.hipMemcpy(p, data, size, 1) == 0          # host -> device
+        ptrs.append(p)
+        return p.value
+
+    try:
+        d_s, d_p, d_m = dev(S, len(S)), dev(P, len(P)), dev(M, len(M))
+        d_o = dev(ctypes.cast(offs, ctypes.c_void_p), 8 * (n + 1))
+        d_c, d_b = dev(None, n), dev(None, 8 * (n // 64))
+        ctx.verify_device(n, d_s, d_p, d_m, d_o, d_c, d_b)
+        assert hip.hipDeviceSynchronize() == 0
+        codes = (ctypes.c_uint8 * n)()
+        words = (ctypes.c_uint64 * (n // 64))()
+        assert hip.hipMemcpy(codes, ctypes.c_void_p(d_c), n, 2) == 0   # device -> host
+        assert hip.hipMemcpy(words, ctypes.c_void_p(d_b), 8 * (n // 64), 2) == 0
+    finally:
+        for p in ptrs:
+            hip.hipFree(p)
+    assert bytes(codes) == expect
+    assert list(words) == ewords
 
 
 def test_adversarial_mix_exact_codes(ctx, vectors):

@@ -214,6 +214,17 @@ def main():
     p28 = [(P >> (28 * i)) & 0xFFFFFFF for i in range(14)]
     w("CESS_CONST uint32_t P28[14] = {" + ", ".join(f"0x{x:07x}u" for x in p28) + "};")
     w(f"CESS_CONST uint32_t PINV28 = 0x{(-pow(P, -1, 1 << 28)) % (1 << 28):07x}u;")
+    # lazy Fp2 product: column-wise multiple of p dominating every column of a
+    # product of two values < 2^384 in 14 x 28-bit limbs (top limb < 2^20)
+    L = [(1 << 28) - 1] * 13 + [(1 << 20) - 1]
+    B = [sum(L[i] * L[k - i] for i in range(14) if 0 <= k - i < 14) for k in range(27)]
+    D = sum(b << (28 * k) for k, b in enumerate(B))
+    adj = (-D) % P
+    for k in range(14):
+        B[k] += (adj >> (28 * k)) & ((1 << 28) - 1)
+    M = sum(b << (28 * k) for k, b in enumerate(B))
+    assert M % P == 0 and M < (1 << 770) and max(B) < (1 << 60)
+    w("CESS_CONST uint64_t LAZY_M28[27] = {" + ", ".join(f"0x{x:016x}ull" for x in B) + "};")
     arr("HALF", mont((P + 1) // 2))
     arr("P_HALF_RAW", (P - 1) // 2)
     # exponents (raw integers, little-endian words)

@@ -18,6 +18,13 @@ extern "C" {
 void emu_fp_mul(const uint32_t* a, const uint32_t* b, uint32_t* out) {
   store_raw(mul(to_mont(load_raw(a)), to_mont(load_raw(b))), out);
 }
+// Montgomery-domain Fp2 product on raw (possibly unreduced, < 2^384) limbs
+void emu_fp2_mul_mont(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
+                      uint32_t* out0, uint32_t* out1) {
+  fp2 r = mul(fp2{load_raw(a0), load_raw(a1)}, fp2{load_raw(b0), load_raw(b1)});
+  memcpy(out0, r.c0.v, 48);
+  memcpy(out1, r.c1.v, 48);
+}
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
 int emu_fp2_sqrt(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {
   fp2 a = {to_mont(load_raw(a0)), to_mont(load_raw(a1))}, r;
@@ -80,11 +87,11 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
   be_words(sig, 12, ws);
   be_words(pk, 24, wp);
   auto snap = [&](int st) {
-    out[2 * st] = g_mul_count;
+    out[2 * st] = 2 * g_mul_count + 5 * g_mul2_count;   // half-multiplies
     out[2 * st + 1] = g_sqr_count;
-    g_mul_count = g_sqr_count = 0;
+    g_mul_count = g_sqr_count = g_mul2_count = 0;
   };
-  g_mul_count = g_sqr_count = 0;
+  g_mul_count = g_sqr_count = g_mul2_count = 0;
   g1a s;
   g1_decompress(ws, s);
   snap(0);

@@ -80,3 +80,27 @@ def test_fp2_sqrt_against_oracle(emu):
             assert o.f2_sqr((val(r0), val(r1))) == tuple(x % o.P for x in a)
         seen[ok] += 1
     assert seen[True] > 50 and seen[False] > 20
+
+
+def test_fp2_mul_lazy_bounds(emu):
+    """The lazily reduced Fp2 product (field.hpp mul(fp2, fp2): one Montgomery
+    reduction per component over combined column sums) at the extremes of its
+    input contract -- components up to 2^384 - 1 (unreduced add_nr sums), 0,
+    p, multiples of p -- and random values; output must be fully reduced."""
+    import random
+
+    import oracle.bls_oracle as o
+    P, RINV = o.P, pow(2, -392, o.P)
+    rng = random.Random(7)
+    limbs = lambda v: (ctypes.c_uint32 * 12)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+    val = lambda arr: sum(arr[i] << (32 * i) for i in range(12))
+    top = (1 << 384) - 1
+    edge = [0, 1, P - 1, P, 2 * P - 1, 4 * P - 1, 8 * P - 1, top, top - 1, 1 << 383, (1 << 364) - 1]
+    cases = [(rng.choice(edge), rng.choice(edge), rng.choice(edge), rng.choice(edge)) for _ in range(200)]
+    cases += [(top, 0, top, top), (0, top, top, top), (top, top, top, top), (0, top, 0, top)]
+    cases += [tuple(rng.randrange(1 << 384) for _ in range(4)) for _ in range(200)]
+    for a0, a1, b0, b1 in cases:
+        r0, r1 = (ctypes.c_uint32 * 12)(), (ctypes.c_uint32 * 12)()
+        emu.emu_fp2_mul_mont(limbs(a0), limbs(a1), limbs(b0), limbs(b1), r0, r1)
+        assert val(r0) == (a0 * b0 - a1 * b1) * RINV % P, (a0, a1, b0, b1)
+        assert val(r1) == (a0 * b1 + a1 * b0) * RINV % P, (a0, a1, b0, b1)

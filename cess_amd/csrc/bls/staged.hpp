@@ -265,10 +265,57 @@ enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6
       /* t3 = frob2(t3 * t0) * t1 * t6 * t4 */ {FE_LOAD, SL_T3}, {FE_MUL, SL_T0}, {FE_FROB, 2}, {FE_MUL, SL_T1},  \
       {FE_MUL, SL_T6}, {FE_MUL, SL_T4}, {FE_END, 0}
 
+// n cyclotomic squarings of acc with z2..z5 in registers and z0, z1 (plus one
+// Fp2 temporary) parked in a 3-Fp2 store `pk` (LDS in k_final): the register
+// working set drops by 72 dwords, which is what the two-waves-per-SIMD budget
+// (256 VGPRs) lacks for the value-based run (measured: 270 -> 119 scratch
+// accesses per squaring).  Same formulas as cyclotomic_square (field.hpp):
+// pair (z0, z1) updates itself; the square of (z2, z3) updates z4, z5 and the
+// square of (z4, z5) updates z2, z3, so the latter is taken first and its t3
+// parked while the former runs.
+// store index: z0 = 0, z4 = 1, z3 = 2, z2 = 3, z1 = 4, z5 = 5
+template <class A, class P>
+CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
+  pk.st(0, acc.ld(0));
+  pk.st(1, acc.ld(4));
+  fp2 z2 = acc.ld(3), z3 = acc.ld(2), z4 = acc.ld(1), z5 = acc.ld(5);
+#pragma unroll 1
+  for (int r = 0; r < n; r++) {
+    CESS_MEMBAR();
+    {
+      const fp2 a = pk.ld(0), b = pk.ld(1);
+      fp2 t0, t1;
+      fp4_square(t0, t1, a, b);
+      pk.st(0, add(dbl(sub(t0, a)), t0));
+      pk.st(1, add(dbl(add(t1, b)), t1));
+    }
+    CESS_MEMBAR();
+    fp2 u0, u1;
+    fp4_square(u0, u1, z4, z5);
+    pk.st(2, u1);
+    CESS_MEMBAR();
+    fp2 t0, t1;
+    fp4_square(t0, t1, z2, z3);
+    z4 = add(dbl(sub(t0, z4)), t0);
+    z5 = add(dbl(add(t1, z5)), t1);
+    const fp2 n3 = mul_nr(pk.ld(2));
+    z2 = add(dbl(add(n3, z2)), n3);
+    z3 = add(dbl(sub(u0, z3)), u0);
+  }
+  CESS_MEMBAR();
+  acc.st(0, pk.ld(0));
+  acc.st(4, pk.ld(1));
+  acc.st(3, z2);
+  acc.st(2, z3);
+  acc.st(1, z4);
+  acc.st(5, z5);
+}
+
 // Run the program.  `acc` is the accumulator store; slot(s) returns the store
-// of slot s (slot SL_F holds the Miller-loop output on entry).  Result in acc.
-template <class A, class SlotFn>
-CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& slot) {
+// of slot s (slot SL_F holds the Miller-loop output on entry); `pk` is the
+// parking store of cyc_square_run_parked.  Result in acc.
+template <class A, class SlotFn, class P>
+CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& slot, const P& pk) {
 #pragma unroll 1
   for (int pc = 0;; pc++) {
     const uint8_t op = prog[pc][0], arg = prog[pc][1];
@@ -278,7 +325,9 @@ CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& s
       case FE_STORE: copy12(slot(arg), acc); break;
       case FE_MUL: mul12(acc, slot(arg)); break;
       case FE_SQN: {
-#if defined(CESS_FE_SQN_REGS)
+#if defined(CESS_FE_SQN_PARK)
+        cyc_square_run_parked(acc, pk, arg);
+#elif defined(CESS_FE_SQN_REGS)
         // square run with the accumulator held in registers (one load/store per run)
         fp12 t;
         fp2* e = &t.c0.c0;

@@ -2,11 +2,12 @@
 // k_final: final exponentiation -> code 0/5 + verdict bitmap (src/lib.rs:93-99, A13/A14)
 //
 // The exponentiation runs as a short program (bls/staged.hpp CESS_FE_PROGRAM)
-// over an accumulator held in LDS (144 KiB image for the block's 256 lanes) and
-// seven HBM slots (uint4 SoA, stride = context capacity) for the cold Fp12
-// temporaries; the Miller-loop output is slot SL_F.
+// over an accumulator in an eighth HBM slot and seven HBM slots (uint4 SoA,
+// stride = context capacity) for the cold Fp12 temporaries; the Miller-loop
+// output is slot SL_F.  Cyclotomic square runs hold the accumulator in
+// registers, with a third of it parked in LDS (two waves per SIMD).
 #include <hip/hip_runtime.h>
-#define CESS_FE_SQN_REGS 1
+#define CESS_FE_SQN_PARK 1
 #include "soa.hpp"
 
 using namespace bls;
@@ -18,6 +19,9 @@ __constant__ uint8_t kFeProgram[][2] = {CESS_FE_PROGRAM};
 // (two waves per SIMD) or the LDS image (one wave per SIMD).
 #ifndef CESS_FINAL_HBM
 #define CESS_FINAL_HBM 1
+#endif
+#if !CESS_FINAL_HBM && defined(CESS_FE_SQN_PARK)
+#error "the LDS accumulator (144 KiB) leaves no room for the square-run parking store"
 #endif
 #if CESS_FINAL_HBM
 #define CESS_LB_F12 __launch_bounds__(256, 2)
@@ -39,9 +43,12 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
       __shared__ uint4 F[36][256];
       LdsF12 acc{F, threadIdx.x};
 #endif
-      final_exp_staged(acc, kFeProgram, [&](int s) {
-        return GlobF12{s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride, stride, i};
-      });
+      // 18 uint4 rows x 256 lanes = 72 KiB per block: two blocks per CU
+      __shared__ uint4 park[18][256];
+      final_exp_staged(
+          acc, kFeProgram,
+          [&](int s) { return GlobF12{s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride, stride, i}; },
+          LdsF12{park, threadIdx.x});
       if (!is_one12(acc)) c = CODE_PAIRING;
       if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
 #pragma unroll 1

@@ -2,6 +2,7 @@
 // (CESS_HOSTEMU) so tests can check the kernel algorithms against the oracle on
 // a machine without a GPU.  Never linked into the product library.
 #include <string.h>
+#define CESS_FE_SQN_PARK 1   // the square-run variant k_final uses
 #include "../../cess_amd/csrc/bls/h2c.hpp"
 #include "../../cess_amd/csrc/bls/staged.hpp"
 
@@ -136,7 +137,8 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   pts[1] = h;
   miller_loop2_staged(ArrF12{&slots[SL_F]}, !s.inf, !(q.inf || h.inf), [](int pair) { return pts[pair]; },
                       [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
-  final_exp_staged(ArrF12{&acc}, prog, [](int sl) { return ArrF12{&slots[sl]}; });
+  static fp12 park;
+  final_exp_staged(ArrF12{&acc}, prog, [](int sl) { return ArrF12{&slots[sl]}; }, ArrF12{&park});
   fp12 g = acc;
   (void)f;
   if (gt_out) {

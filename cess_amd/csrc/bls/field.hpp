@@ -1,7 +1,11 @@
 // BLS12-381 field tower for CDNA4 (gfx950): Fp, Fp2, Fp6, Fp12.
 //
 // Representation: 12 x u32 little-endian limbs (cheap carry-chain add/sub),
-// Montgomery form with R = 2^392, every value fully reduced (< p).
+// Montgomery form with R = 2^392, values kept in the redundant range [0, 2p):
+// a Montgomery product of inputs < 8p is already < 2p, so no multiply pays for a
+// final conditional subtraction; add/sub/neg work modulo 2p with the same
+// instruction count as modulo p, and only eq/is_zero/from_mont (comparisons and
+// serialisation) bring a value to its canonical form < p.
 //
 // Hot primitive: product-scanning (Comba) Montgomery multiplication computed in
 // 14 x 28-bit limbs.  Each column of 28-bit products fits a 64-bit accumulator
@@ -111,7 +115,7 @@ CESS_HD uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
 }
 #endif
 
-// r = t - p if t >= p  (t < 2p)
+// r = t - p if t >= p  (t < 2p): canonical form
 CESS_HD fp fp_reduce_once(const fp& t) {
   fp s;
   uint32_t borrow = 0;
@@ -123,12 +127,24 @@ CESS_HD fp fp_reduce_once(const fp& t) {
   return r;
 }
 
+// r = t - 2p if t >= 2p  (t < 4p): back into [0, 2p)
+CESS_HD fp fp_reduce2(const fp& t) {
+  fp s;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) s.v[i] = subc32(t.v[i], c::P2_RAW[i], borrow, &borrow);
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = borrow ? t.v[i] : s.v[i];
+  return r;
+}
+
 CESS_HD fp add(const fp& a, const fp& b) {
   fp t;
   uint32_t carry = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) t.v[i] = addc32(a.v[i], b.v[i], carry, &carry);
-  return fp_reduce_once(t);  // a + b < 2p < 2^382: no carry out of limb 11
+  return fp_reduce2(t);  // a + b < 4p < 2^383: no carry out of limb 11
 }
 
 CESS_HD fp sub(const fp& a, const fp& b) {
@@ -136,18 +152,18 @@ CESS_HD fp sub(const fp& a, const fp& b) {
   uint32_t borrow = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) t.v[i] = subc32(a.v[i], b.v[i], borrow, &borrow);
-  // if borrow: add p back
+  // if borrow: add 2p back (a - b > -2p)
   const uint32_t mask = 0u - borrow;
   uint32_t carry = 0;
   fp r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.v[i] = addc32(t.v[i], c::P_RAW[i] & mask, carry, &carry);
+  for (int i = 0; i < 12; i++) r.v[i] = addc32(t.v[i], c::P2_RAW[i] & mask, carry, &carry);
   return r;
 }
 
-// Unreduced sum (no conditional subtraction): a + b < 2^384 for a, b < 2^383.
+// Unreduced sum (no conditional subtraction): a + b < 4p for a, b < 2p.
 // ONLY for values consumed by mul(): the Montgomery product accepts inputs up to
-// 8p (a*b < 64 p^2 < p R, R = 2^392) and returns a fully reduced value.  Never
+// 8p (a*b < 64 p^2 < p R, R = 2^392) and returns a value < 2p.  Never
 // feed an unreduced value to sub/neg/sqr/eq or store it.
 CESS_HD fp add_nr(const fp& a, const fp& b) {
   fp t;
@@ -159,26 +175,30 @@ CESS_HD fp add_nr(const fp& a, const fp& b) {
 
 CESS_HD fp dbl(const fp& a) { return add(a, a); }
 
+// a = 0 mod p, for a in [0, 2p): a is 0 or p
 CESS_HD bool is_zero(const fp& a) {
-  uint32_t acc = 0;
+  uint32_t z = 0, q = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) acc |= a.v[i];
-  return acc == 0;
+  for (int i = 0; i < 12; i++) z |= a.v[i], q |= a.v[i] ^ c::P_RAW[i];
+  return z == 0 || q == 0;
 }
 
 CESS_HD fp neg(const fp& a) {
-  // p - a, and 0 -> 0
+  // 2p - a, and 0 -> 0 (p stays p: both represent 0)
   fp r;
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.v[i] = subc32(c::P_RAW[i], a.v[i], borrow, &borrow);
-  bool z = is_zero(a);
+  for (int i = 0; i < 12; i++) r.v[i] = subc32(c::P2_RAW[i], a.v[i], borrow, &borrow);
+  uint32_t z = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.v[i] = z ? 0u : r.v[i];
+  for (int i = 0; i < 12; i++) z |= a.v[i];
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = z == 0 ? 0u : r.v[i];
   return r;
 }
 
-CESS_HD bool eq(const fp& a, const fp& b) {
+CESS_HD bool eq(const fp& a0, const fp& b0) {
+  const fp a = fp_reduce_once(a0), b = fp_reduce_once(b0);
   uint32_t acc = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) acc |= a.v[i] ^ b.v[i];
@@ -271,7 +291,7 @@ CESS_HD fp mont28(Col&& col) {
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;   // result < 2p < 2^382: fits
-  return fp_reduce_once(pack28(t));
+  return pack28(t);
 }
 
 // Two Montgomery reductions side by side (lazy Fp2 product):
@@ -310,8 +330,8 @@ CESS_HD void mont28x2(Col&& col, fp& out0, fp& out1) {
   }
   t0[13] = (uint32_t)acc0;
   t1[13] = (uint32_t)acc1;
-  out0 = fp_reduce_once(pack28(t0));
-  out1 = fp_reduce_once(pack28(t1));
+  out0 = pack28(t0);
+  out1 = pack28(t1);
 }
 
 // a * b * 2^-392 mod p
@@ -358,11 +378,11 @@ CESS_HD fp mul3(const fp& a) { return add(dbl(a), a); }
 CESS_HD fp mul4(const fp& a) { return dbl(dbl(a)); }
 CESS_HD fp mul8(const fp& a) { return dbl(dbl(dbl(a))); }
 
-// canonical integer <-> Montgomery
+// canonical integer <-> Montgomery (a * 1 / R <= p: one subtraction canonicalises)
 CESS_HD fp from_mont(const fp& a) {
   fp one_raw = fp_zero();
   one_raw.v[0] = 1;
-  return mul(a, one_raw);
+  return fp_reduce_once(mul(a, one_raw));
 }
 CESS_HD fp to_mont(const fp& a_raw) { return mul(a_raw, fp_from(c::R2)); }
 
@@ -449,8 +469,8 @@ CESS_HD fp2 add(const fp2& a, const fp2& b) {
   }
 #pragma unroll
   for (int i = 0; i < 12; i++) {
-    s0.v[i] = subc32(t0.v[i], c::P_RAW[i], b0, &b0);
-    s1.v[i] = subc32(t1.v[i], c::P_RAW[i], b1, &b1);
+    s0.v[i] = subc32(t0.v[i], c::P2_RAW[i], b0, &b0);
+    s1.v[i] = subc32(t1.v[i], c::P2_RAW[i], b1, &b1);
   }
   fp2 r;
 #pragma unroll
@@ -472,8 +492,8 @@ CESS_HD fp2 sub(const fp2& a, const fp2& b) {
   fp2 r;
 #pragma unroll
   for (int i = 0; i < 12; i++) {
-    r.c0.v[i] = addc32(t0.v[i], c::P_RAW[i] & m0, c0, &c0);
-    r.c1.v[i] = addc32(t1.v[i], c::P_RAW[i] & m1, c1, &c1);
+    r.c0.v[i] = addc32(t0.v[i], c::P2_RAW[i] & m0, c0, &c0);
+    r.c1.v[i] = addc32(t1.v[i], c::P2_RAW[i] & m1, c1, &c1);
   }
   return r;
 }

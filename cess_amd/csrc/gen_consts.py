@@ -208,6 +208,7 @@ def main():
         w(f"CESS_CONST uint32_t {name}[{n}] = {{" + ", ".join(f"0x{x:08x}u" for x in limbs(v, n)) + "};")
 
     arr("P_RAW", P)
+    arr("P2_RAW", 2 * P)   # field values live in [0, 2p) (field.hpp)
     arr("ONE", mont(1))
     arr("R2", RM * RM % P)
     arr("R2_384", (1 << 384) * RM * RM % P)   # mul(H, .) = H * 2^384 * R

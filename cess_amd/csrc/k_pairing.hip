@@ -18,17 +18,34 @@ __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_af
   g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); });
 }
 
-// Miller accumulator placement: CESS_MILLER_HBM=1 keeps each lane's Fp12 in its
-// HBM output slot (L2/MALL-resident) so two waves fit per SIMD; 0 keeps it in
-// an LDS image (144 dwords x 256 lanes = 144 KiB, one wave per SIMD).
-#ifndef CESS_MILLER_HBM
-#define CESS_MILLER_HBM 0
+// Miller accumulator placement (CESS_MILLER_MODE):
+//   0: an LDS image (144 dwords x 256 lanes = 144 KiB, one wave per SIMD);
+//   1: the lane's HBM output slot (L2/MALL-resident), two waves per SIMD;
+//   2: split -- the c0 half (72 dwords) in LDS, the c1 half in the HBM output
+//      slot: 72 KiB per block, two blocks (two waves per SIMD) per CU.
+#ifndef CESS_MILLER_MODE
+#define CESS_MILLER_MODE 0
 #endif
-#if CESS_MILLER_HBM
+#if CESS_MILLER_MODE
 #define CESS_LB_F12 __launch_bounds__(256, 2)
 #else
 #define CESS_LB_F12 __launch_bounds__(256, 1)
 #endif
+
+// Fp12 store with the c0 half (store indices 0-2) in LDS and the c1 half (3-5)
+// in HBM.  Indices are compile-time in the unrolled operations; the rolled
+// copy loops branch wave-uniformly.
+struct SplitF12 {
+  LdsF12 lo;
+  GlobF12 hi;
+  CESS_HD fp2 ld(int k) const { return k < 3 ? lo.ld(k) : hi.ld(k); }
+  CESS_HD void st(int k, const fp2& a) const {
+    if (k < 3)
+      lo.st(k, a);
+    else
+      hi.st(k, a);
+  }
+};
 
 __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ code,
                                      const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
@@ -39,8 +56,11 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   if (i >= n) return;
   if (code[i] != 0) return;
   uint8_t fl = inf[i];
-#if CESS_MILLER_HBM
+#if CESS_MILLER_MODE == 1
   GlobF12 f{fout, stride, i};
+#elif CESS_MILLER_MODE == 2
+  __shared__ uint4 F[18][256];
+  SplitF12 f{LdsF12{F, threadIdx.x}, GlobF12{fout, stride, i}};
 #else
   __shared__ uint4 F[36][256];
   LdsF12 f{F, threadIdx.x};
@@ -54,7 +74,10 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
         return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
       },
       [&](int pair, int k) { return pair ? ld_coeff4(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k); });
-#if !CESS_MILLER_HBM
+#if CESS_MILLER_MODE == 2
+#pragma unroll 1
+  for (int k = 0; k < 3; k++) f.hi.st(k, f.lo.ld(k));
+#elif CESS_MILLER_MODE == 0
   copy12(GlobF12{fout, stride, i}, f);
 #endif
 }

@@ -23,8 +23,9 @@ void emu_fp_mul(const uint32_t* a, const uint32_t* b, uint32_t* out) {
 void emu_fp2_mul_mont(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
                       uint32_t* out0, uint32_t* out1) {
   fp2 r = mul(fp2{load_raw(a0), load_raw(a1)}, fp2{load_raw(b0), load_raw(b1)});
-  memcpy(out0, r.c0.v, 48);
-  memcpy(out1, r.c1.v, 48);
+  const fp c0 = fp_reduce_once(r.c0), c1 = fp_reduce_once(r.c1);   // [0, 2p) -> canonical
+  memcpy(out0, c0.v, 48);
+  memcpy(out1, c1.v, 48);
 }
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
 int emu_fp2_sqrt(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {

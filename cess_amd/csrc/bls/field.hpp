@@ -386,22 +386,38 @@ CESS_HD fp from_mont(const fp& a) {
 }
 CESS_HD fp to_mont(const fp& a_raw) { return mul(a_raw, fp_from(c::R2)); }
 
-// a^e for a fixed 12-word exponent (square-and-multiply, MSB first).
-// The branch on the exponent bit is wave-uniform.
+// a^e for a fixed 12-word exponent: MSB-first sliding window of width 3 over
+// the odd powers a, a^3, a^5, a^7 (table held in registers; the window is
+// picked with uniform selects, not a dynamically indexed array, so nothing goes
+// to scratch).  For the 379-381-bit exponents used here (p-2, (p+1)/4,
+// (p-3)/4; ~229 set bits) this is ~110 multiplies instead of ~229.  All
+// branches depend on the exponent only, so they are wave-uniform.
+CESS_HD uint32_t exp_bit(const uint32_t (&e)[12], int i) { return (e[i >> 5] >> (i & 31)) & 1u; }
 CESS_HD fp pow_fixed(const fp& a, const uint32_t (&e)[12]) {
+  const fp a2 = sqr(a);
+  const fp t1 = a, t3 = mul(t1, a2), t5 = mul(t3, a2), t7 = mul(t5, a2);
   fp r = fp_one();
   bool started = false;
+  int i = 383;
 #pragma unroll 1
-  for (int w = 11; w >= 0; w--) {
-    uint32_t word = e[w];
-#pragma unroll 1
-    for (int b = 31; b >= 0; b--) {
+  while (i >= 0) {
+    if (!exp_bit(e, i)) {
       if (started) r = sqr(r);
-      if ((word >> b) & 1u) {
-        r = started ? mul(r, a) : a;
-        started = true;
-      }
+      i--;
+      continue;
     }
+    int j = i >= 2 ? i - 2 : 0;   // window e[i..j], j the lowest set bit in it
+    while (!exp_bit(e, j)) j++;
+    uint32_t v = 0;
+#pragma unroll 1
+    for (int k = i; k >= j; k--) {
+      v = 2 * v + exp_bit(e, k);
+      if (started) r = sqr(r);
+    }
+    const fp t = v == 1 ? t1 : v == 3 ? t3 : v == 5 ? t5 : t7;
+    r = started ? mul(r, t) : t;
+    started = true;
+    i = j - 1;
   }
   return r;
 }
@@ -531,6 +547,18 @@ CESS_HD fp2 mul8(const fp2& a) { return {mul8(a.c0), mul8(a.c1)}; }
 //                       each column of t is exactly v0 + v1 + cross terms).
 // c0 < 2^770 < p 2^392, so each reduction returns < 2p.  3 x 196 product +
 // 2 x 196 reduction mads = 980 vs 1176 for three separate products.
+#ifndef CESS_FP2_MUL_LAZY
+#define CESS_FP2_MUL_LAZY 1
+#endif
+#if !CESS_FP2_MUL_LAZY
+// Karatsuba with three separately reduced products (fewer live registers than
+// the lazy form below: for kernels that run two waves per SIMD)
+CESS_HD fp2 mul(const fp2& a, const fp2& b) {
+  fp v0 = mul(a.c0, b.c0), v1 = mul(a.c1, b.c1);
+  fp t = mul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1));
+  return {sub(v0, v1), sub(sub(t, v0), v1)};
+}
+#else
 CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   CESS_COUNT_MUL2();
   fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1;
@@ -568,6 +596,7 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   seq(r.c1);
   return r;
 }
+#endif
 CESS_HD fp2 sqr(const fp2& a) {   // a must be reduced (sub below)
   fp t0 = mul(add_nr(a.c0, a.c1), sub(a.c0, a.c1));
   fp t1 = mul(a.c0, a.c1);

@@ -104,3 +104,25 @@ def test_fp2_mul_lazy_bounds(emu):
         emu.emu_fp2_mul_mont(limbs(a0), limbs(a1), limbs(b0), limbs(b1), r0, r1)
         assert val(r0) == (a0 * b0 - a1 * b1) * RINV % P, (a0, a1, b0, b1)
         assert val(r1) == (a0 * b1 + a1 * b0) * RINV % P, (a0, a1, b0, b1)
+
+
+def test_cpu_baseline_path_codes(vectors):
+    """bench.py's cpu_baseline leg (tests/hostemu/cpu_verify.cpp, multi-threaded)
+    gives the golden verdict codes for every fixed-size case."""
+    src = os.path.join(HERE, "hostemu", "cpu_verify.cpp")
+    lib = os.path.join(HERE, "hostemu", "libcpu_verify.so")
+    hdr_dir = os.path.join(HERE, "..", "cess_amd", "csrc", "bls")
+    newest = max([os.path.getmtime(src)] + [os.path.getmtime(os.path.join(hdr_dir, f)) for f in os.listdir(hdr_dir)])
+    if not os.path.exists(lib) or os.path.getmtime(lib) < newest:
+        subprocess.check_call(["g++", "-O3", "-std=c++17", "-DCESS_HOSTEMU", "-shared", "-fPIC", "-pthread", src,
+                               "-o", lib])
+    cpu = ctypes.CDLL(lib)
+    cases = [c for c in vectors["cases"] if len(c["sig"]) == 96 and len(c["pk"]) == 192 and len(c["msg"]) == 64]
+    assert len(cases) >= 4
+    n = len(cases)
+    sigs = b"".join(bytes.fromhex(c["sig"]) for c in cases)
+    msgs = b"".join(bytes.fromhex(c["msg"]) for c in cases)
+    pks = b"".join(bytes.fromhex(c["pk"]) for c in cases)
+    codes = (ctypes.c_uint8 * n)()
+    cpu.cpu_verify_batch(ctypes.c_uint64(n), sigs, msgs, ctypes.c_uint32(32), pks, codes, ctypes.c_int(4))
+    assert list(codes) == [c["code"] for c in cases]

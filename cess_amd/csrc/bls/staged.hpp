@@ -177,6 +177,48 @@ CESS_HD void mul12(const S& f, const G& g) {
   st6(f, 0, add(t0, mul_v(t1)));
 }
 
+// Fp6 product a * b with the operands' Fp2 pieces fetched on demand (a(j),
+// b(j): loaders, typically loads from a store) and each coefficient of the
+// result handed to sink(j, c_j) as soon as it is complete.  Only the three
+// diagonal products stay in registers (72 dwords); the value-based mul(fp6,
+// fp6) keeps both 72-dword operands live as well, which spills at two waves
+// per SIMD.  Loaders may return unreduced sums (< 4p); sums of two of them
+// (< 8p) still satisfy mul()'s input bound.
+template <class LA, class LB, class SK>
+CESS_HD void mul6_stream(LA&& a, LB&& b, SK&& sink) {
+  const fp2 v0 = mul(a(0), b(0));
+  CESS_MEMBAR();
+  const fp2 v1 = mul(a(1), b(1));
+  CESS_MEMBAR();
+  const fp2 v2 = mul(a(2), b(2));
+  CESS_MEMBAR();
+  sink(0, add(mul_nr(sub(sub(mul(add_nr(a(1), a(2)), add_nr(b(1), b(2))), v1), v2)), v0));
+  CESS_MEMBAR();
+  sink(1, add(sub(sub(mul(add_nr(a(0), a(1)), add_nr(b(0), b(1))), v0), v1), mul_nr(v2)));
+  CESS_MEMBAR();
+  sink(2, add(sub(sub(mul(add_nr(a(0), a(2)), add_nr(b(0), b(2))), v0), v2), v1));
+  CESS_MEMBAR();
+}
+
+// d <- f * g (Karatsuba over Fp6) with every operand streamed: d must be a
+// store distinct from f and g; t is a one-Fp6 temporary store (3 Fp2, indices
+// 0-2).  t0 = f0 g0 goes to t, t1 = f1 g1 to d.c1, then d.c0 = t0 + v t1 and
+// d.c1 = (f0 + f1)(g0 + g1) - t0 - t1 in place.
+template <class D, class S, class G, class T>
+CESS_HD void mul12_stream(const D& d, const S& f, const G& g, const T& t) {
+  mul6_stream([&](int j) { return f.ld(j); }, [&](int j) { return g.ld(j); },
+              [&](int j, const fp2& v) { t.st(j, v); });
+  mul6_stream([&](int j) { return f.ld(3 + j); }, [&](int j) { return g.ld(3 + j); },
+              [&](int j, const fp2& v) { d.st(3 + j, v); });
+  d.st(0, add(t.ld(0), mul_nr(d.ld(5))));
+  d.st(1, add(t.ld(1), d.ld(3)));
+  d.st(2, add(t.ld(2), d.ld(4)));
+  CESS_MEMBAR();
+  mul6_stream([&](int j) { return add_nr(f.ld(j), f.ld(3 + j)); },
+              [&](int j) { return add_nr(g.ld(j), g.ld(3 + j)); },
+              [&](int j, const fp2& x) { d.st(3 + j, sub(sub(x, t.ld(j)), d.ld(3 + j))); });
+}
+
 // f <- f^2 for f in the cyclotomic subgroup (Granger-Scott, eprint 2009/565)
 template <class S>
 CESS_HD void cycsq12(const S& f) {
@@ -311,19 +353,28 @@ CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
   acc.st(5, z5);
 }
 
-// Run the program.  `acc` is the accumulator store; slot(s) returns the store
-// of slot s (slot SL_F holds the Miller-loop output on entry); `pk` is the
-// parking store of cyc_square_run_parked.  Result in acc.
+// Run the program.  The accumulator alternates between the stores acc0 and
+// acc1: FE_MUL writes the product of the current one and a slot into the other
+// (mul12_stream, with the parking store `pk` as its Fp6 temporary); every other
+// opcode works in place.  slot(s) returns the store of slot s (slot SL_F holds
+// the Miller-loop output on entry); `pk` is also the parking store of
+// cyc_square_run_parked.  Returns the index (0/1) of the store holding the
+// result.
 template <class A, class SlotFn, class P>
-CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& slot, const P& pk) {
+CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)[2], SlotFn&& slot, const P& pk) {
+  int cur = 0;
 #pragma unroll 1
   for (int pc = 0;; pc++) {
     const uint8_t op = prog[pc][0], arg = prog[pc][1];
     if (op == FE_END) break;
+    const A& acc = cur ? acc1 : acc0;
     switch (op) {
       case FE_LOAD: copy12(acc, slot(arg)); break;
       case FE_STORE: copy12(slot(arg), acc); break;
-      case FE_MUL: mul12(acc, slot(arg)); break;
+      case FE_MUL:
+        mul12_stream(cur ? acc0 : acc1, acc, slot(arg), pk);
+        cur ^= 1;
+        break;
       case FE_SQN: {
 #if defined(CESS_FE_SQN_PARK)
         cyc_square_run_parked(acc, pk, arg);
@@ -349,6 +400,7 @@ CESS_HD void final_exp_staged(const A& acc, const uint8_t (*prog)[2], SlotFn&& s
       default: break;
     }
   }
+  return cur;
 }
 
 // Miller loop for the two pairs of PublicKey::verify on an accumulator store:

@@ -2,9 +2,9 @@
 // k_final: final exponentiation -> code 0/5 + verdict bitmap (src/lib.rs:93-99, A13/A14)
 //
 // The exponentiation runs as a short program (bls/staged.hpp CESS_FE_PROGRAM)
-// over an accumulator in an eighth HBM slot and seven HBM slots (uint4 SoA,
-// stride = context capacity) for the cold Fp12 temporaries; the Miller-loop
-// output is slot SL_F.  Cyclotomic square runs hold the accumulator in
+// over two ping-pong accumulators (HBM slots 8 and 9) and seven HBM slots
+// (uint4 SoA, stride = context capacity) for the cold Fp12 temporaries; the
+// Miller-loop output is slot SL_F.  Cyclotomic square runs hold the accumulator in
 // registers, with a third of it parked in LDS (two waves per SIMD).
 #include <hip/hip_runtime.h>
 #define CESS_FE_SQN_PARK 1
@@ -15,19 +15,7 @@ using namespace cess;
 
 __constant__ uint8_t kFeProgram[][2] = {CESS_FE_PROGRAM};
 
-// Accumulator placement as in k_miller (CESS_FINAL_HBM): an eighth HBM slot
-// (two waves per SIMD) or the LDS image (one wave per SIMD).
-#ifndef CESS_FINAL_HBM
-#define CESS_FINAL_HBM 1
-#endif
-#if !CESS_FINAL_HBM && defined(CESS_FE_SQN_PARK)
-#error "the LDS accumulator (144 KiB) leaves no room for the square-run parking store"
-#endif
-#if CESS_FINAL_HBM
 #define CESS_LB_F12 __launch_bounds__(256, 2)
-#else
-#define CESS_LB_F12 __launch_bounds__(256, 1)
-#endif
 
 __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
                                     uint4* __restrict__ slots, uint64_t* __restrict__ bitmap,
@@ -37,18 +25,16 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
   if (i < n) {
     c = code[i];
     if (c == 0) {
-#if CESS_FINAL_HBM
-      GlobF12 acc{slots + (uint64_t)(SL_N - 1) * 36 * stride, stride, i};
-#else
-      __shared__ uint4 F[36][256];
-      LdsF12 acc{F, threadIdx.x};
-#endif
+      // two HBM accumulators (slots SL_N - 1 and SL_N): FE_MUL ping-pongs
+      GlobF12 acc0{slots + (uint64_t)(SL_N - 1) * 36 * stride, stride, i};
+      GlobF12 acc1{slots + (uint64_t)SL_N * 36 * stride, stride, i};
       // 18 uint4 rows x 256 lanes = 72 KiB per block: two blocks per CU
       __shared__ uint4 park[18][256];
-      final_exp_staged(
-          acc, kFeProgram,
+      const int which = final_exp_staged(
+          acc0, acc1, kFeProgram,
           [&](int s) { return GlobF12{s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride, stride, i}; },
           LdsF12{park, threadIdx.x});
+      const GlobF12 acc = which ? acc1 : acc0;
       if (!is_one12(acc)) c = CODE_PAIRING;
       if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
 #pragma unroll 1

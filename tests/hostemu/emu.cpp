@@ -138,9 +138,10 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   pts[1] = h;
   miller_loop2_staged(ArrF12{&slots[SL_F]}, !s.inf, !(q.inf || h.inf), [](int pair) { return pts[pair]; },
                       [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
-  static fp12 park;
-  final_exp_staged(ArrF12{&acc}, prog, [](int sl) { return ArrF12{&slots[sl]}; }, ArrF12{&park});
-  fp12 g = acc;
+  static fp12 park, acc1;
+  const int which = final_exp_staged(ArrF12{&acc}, ArrF12{&acc1}, prog, [](int sl) { return ArrF12{&slots[sl]}; },
+                                     ArrF12{&park});
+  fp12 g = which ? acc1 : acc;
   (void)f;
   if (gt_out) {
     const fp* e = &g.c0.c0.c0;

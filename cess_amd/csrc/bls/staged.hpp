@@ -219,6 +219,68 @@ CESS_HD void mul12_stream(const D& d, const S& f, const G& g, const T& t) {
               [&](int j, const fp2& x) { d.st(3 + j, sub(sub(x, t.ld(j)), d.ld(3 + j))); });
 }
 
+// d <- f^2 (complex squaring) with streamed operands; d distinct from f, t a
+// one-Fp6 temporary store.  ab = f0 f1 goes to t; d.c0 = (f0 + f1)(f0 + v f1)
+// - ab - v ab, d.c1 = 2 ab.
+template <class D, class S, class T>
+CESS_HD void sqr12_stream(const D& d, const S& f, const T& t) {
+  mul6_stream([&](int j) { return f.ld(j); }, [&](int j) { return f.ld(3 + j); },
+              [&](int j, const fp2& v) { t.st(j, v); });
+  mul6_stream([&](int j) { return add_nr(f.ld(j), f.ld(3 + j)); },
+              [&](int j) { return j == 0 ? add_nr(f.ld(0), mul_nr(f.ld(5))) : add_nr(f.ld(j), f.ld(2 + j)); },
+              [&](int j, const fp2& x) {
+                const fp2 vab = j == 0 ? mul_nr(t.ld(2)) : t.ld(j - 1);
+                d.st(j, sub(sub(x, t.ld(j)), vab));
+              });
+#pragma unroll 1
+  for (int j = 0; j < 3; j++) d.st(3 + j, dbl(t.ld(j)));
+}
+
+// d <- f * (c0 + c1 v + c4 v w) (Fp12::mul_by_014) with streamed operands; d
+// distinct from f, t a one-Fp6 temporary store.  bb = f1 c4 v goes to t,
+// d.c0 = aa + v bb with aa = f0 (c0 + c1 v), and d.c1 = (f0 + f1)(c0 + (c1 +
+// c4) v) - aa - bb, using aa = d.c0 - v bb.
+template <class D, class S, class T>
+CESS_HD void mul014_stream(const D& d, const S& f, const fp2& c0, const fp2& c1, const fp2& c4, const T& t) {
+  t.st(0, mul_nr(mul(f.ld(5), c4)));
+  CESS_MEMBAR();
+  t.st(1, mul(f.ld(3), c4));
+  CESS_MEMBAR();
+  t.st(2, mul(f.ld(4), c4));
+  CESS_MEMBAR();
+  {
+    const fp2 t0 = mul(f.ld(0), c0);
+    CESS_MEMBAR();
+    const fp2 t1 = mul(f.ld(1), c1);
+    CESS_MEMBAR();
+    d.st(1, add(sub(sub(mul(add_nr(f.ld(0), f.ld(1)), add_nr(c0, c1)), t0), t1), t.ld(0)));
+    CESS_MEMBAR();
+    d.st(0, add(add(mul_nr(mul(f.ld(2), c1)), t0), mul_nr(t.ld(2))));
+    CESS_MEMBAR();
+    d.st(2, add(add(mul(f.ld(2), c0), t1), t.ld(1)));
+    CESS_MEMBAR();
+  }
+  const fp2 e = add(c1, c4);
+  const fp2 u0 = mul(add_nr(f.ld(0), f.ld(3)), c0);
+  CESS_MEMBAR();
+  const fp2 u1 = mul(add_nr(f.ld(1), f.ld(4)), e);
+  CESS_MEMBAR();
+  {
+    const fp2 x = sub(sub(mul(add_nr(add_nr(f.ld(0), f.ld(3)), add_nr(f.ld(1), f.ld(4))), add_nr(c0, e)), u0), u1);
+    d.st(4, sub(add(sub(x, d.ld(1)), t.ld(0)), t.ld(1)));       // + v bb_1 - bb_1
+  }
+  CESS_MEMBAR();
+  {
+    const fp2 x = add(mul_nr(mul(add_nr(f.ld(2), f.ld(5)), e)), u0);
+    d.st(3, sub(add(sub(x, d.ld(0)), mul_nr(t.ld(2))), t.ld(0)));
+  }
+  CESS_MEMBAR();
+  {
+    const fp2 x = add(mul(add_nr(f.ld(2), f.ld(5)), c0), u1);
+    d.st(5, sub(add(sub(x, d.ld(2)), t.ld(1)), t.ld(2)));
+  }
+}
+
 // f <- f^2 for f in the cyclotomic subgroup (Granger-Scott, eprint 2009/565)
 template <class S>
 CESS_HD void cycsq12(const S& f) {
@@ -425,6 +487,36 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
     CESS_MEMBAR();
   }
   conj12(f);   // x < 0
+}
+
+// Miller loop with the accumulator ping-ponging between two stores fa, fb
+// (every Fp12 step reads one and writes the other) and one Fp6 temporary t;
+// otherwise as miller_loop2_staged.  Returns the index (0: fa, 1: fb) of the
+// store holding the result.
+template <class S, class T, class Pt, class Src>
+CESS_HD int miller_loop2_pp(const S& fa, const S& fb, const T& t, bool use0, bool use1, Pt&& pt, Src&& src) {
+  set_one12(fa);
+  int cur = 0;
+#pragma unroll 1
+  for (int s = 0; s < N_COEFFS; s++) {
+#pragma unroll 1
+    for (int pair = 0; pair < 2; pair++) {
+      if (!(pair ? use1 : use0)) continue;
+      coeff3 k = src(pair, s);
+      g1a p = pt(pair);
+      fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
+      mul014_stream(cur ? fa : fb, cur ? fb : fa, k.c2, c1, c4, t);
+      cur ^= 1;
+      CESS_MEMBAR();
+    }
+    if (square_after_step(s)) {
+      sqr12_stream(cur ? fa : fb, cur ? fb : fa, t);
+      cur ^= 1;
+    }
+    CESS_MEMBAR();
+  }
+  conj12(cur ? fb : fa);   // x < 0
+  return cur;
 }
 
 }  // namespace bls

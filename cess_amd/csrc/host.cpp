@@ -20,7 +20,7 @@ __global__ void k_decode_pk(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, 
 __global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*, uint32_t*, uint64_t);
 __global__ void k_prepare(uint64_t, const uint32_t*, uint4*, uint64_t);
 __global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                         const uint4*, uint4*, uint64_t);
+                         const uint4*, uint4*, uint4*, uint64_t);
 __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
@@ -79,7 +79,7 @@ struct RlcState {
   bool local_ok = false;
   uint64_t checks = 0, leaves = 0, leaf_sigs = 0;
   DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
-  DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, acc, slots, fin_code, fin_bm, gt, gts, tmp;
+  DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, rec_f2, acc, slots, fin_code, fin_bm, gt, gts, tmp;
   DevBuf seg, part2, rec_coeffs;
 };
 
@@ -232,7 +232,7 @@ static int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* 
   hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
                      (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
                      (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)c->coeffs.as<uint4>(),
-                     c->fval.as<uint4>(), st);
+                     c->fval.as<uint4>(), c->fe_slots.as<uint4>(), st);
   if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
   hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,
                      gt, st);
@@ -482,7 +482,8 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
   int r = 0;
   r |= R.S.ensure((uint64_t)NR * 36 * 4) | R.Qs.ensure((uint64_t)M * 36 * 4);
   r |= R.rec_code.ensure(M) | R.rec_inf.ensure(M) | R.rec_sig.ensure((uint64_t)M * CESS_W_G1 * 4);
-  r |= R.rec_h.ensure((uint64_t)M * CESS_W_G1 * 4) | R.rec_f.ensure((uint64_t)M * CESS_W_FP12 * 4);
+  r |= R.rec_h.ensure((uint64_t)M * CESS_W_G1 * 4) | R.rec_f.ensure((uint64_t)M * CESS_W_FP12 * 4) |
+       R.rec_f2.ensure((uint64_t)M * CESS_W_FP12 * 4);
   r |= R.acc.ensure((uint64_t)NR * CESS_W_FP12 * 4) | R.slots.ensure((uint64_t)NR * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
   r |= R.fin_code.ensure(NR) | R.fin_bm.ensure(((NR + 63) / 64) * 8) | R.gt.ensure((uint64_t)NR * 576);
   if (NR > 1) r |= R.rec_coeffs.ensure((uint64_t)M * CESS_W_COEFFS * 4);
@@ -504,7 +505,8 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
   hipLaunchKernelGGL(k_miller, dim3((M + kBlock - 1) / kBlock), dim3(kBlock), 0, s, (uint64_t)M,
                      (const uint8_t*)R.rec_code.as<uint8_t>(), (const uint8_t*)R.rec_inf.as<uint8_t>(),
                      (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
-                     (const uint32_t*)c->neg_g2.as<uint32_t>(), coeffs, R.rec_f.as<uint4>(), (uint64_t)M);
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), coeffs, R.rec_f.as<uint4>(), R.rec_f2.as<uint4>(),
+                     (uint64_t)M);
   hipLaunchKernelGGL(k_fp12_prod_multi, dim3((NR + 63) / 64), dim3(64), 0, s, NR, K, (const uint4*)R.rec_f.as<uint4>(),
                      R.acc.as<uint4>());
   HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));

@@ -22,7 +22,11 @@ __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_af
 //   0: an LDS image (144 dwords x 256 lanes = 144 KiB, one wave per SIMD);
 //   1: the lane's HBM output slot (L2/MALL-resident), two waves per SIMD;
 //   2: split -- the c0 half (72 dwords) in LDS, the c1 half in the HBM output
-//      slot: 72 KiB per block, two blocks (two waves per SIMD) per CU.
+//      slot: 72 KiB per block, two blocks (two waves per SIMD) per CU;
+//   3: ping-pong -- the accumulator alternates between the HBM output slot and
+//      a second HBM slot (`pp`), every Fp12 step streams its operands
+//      (bls/staged.hpp mul014_stream / sqr12_stream) with one Fp6 temporary in
+//      LDS (72 KiB per block): two waves per SIMD.
 #ifndef CESS_MILLER_MODE
 #define CESS_MILLER_MODE 0
 #endif
@@ -51,12 +55,13 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
                                      const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
                                      const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
                                      const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
-                                     uint64_t stride) {
+                                     uint4* __restrict__ pp, uint64_t stride) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (code[i] != 0) return;
   uint8_t fl = inf[i];
-#if CESS_MILLER_MODE == 1
+#if CESS_MILLER_MODE == 3
+#elif CESS_MILLER_MODE == 1
   GlobF12 f{fout, stride, i};
 #elif CESS_MILLER_MODE == 2
   __shared__ uint4 F[18][256];
@@ -67,17 +72,23 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
 #endif
   // the G1 points are re-read from HBM (L2) for every line instead of being
   // held in 48 registers across the loop
-  miller_loop2_staged(
-      f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0,
-      [&](int pair) {
-        const uint32_t* b = pair ? h_aff : sig_aff;
-        return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
-      },
-      [&](int pair, int k) { return pair ? ld_coeff4(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k); });
+  auto pt = [&](int pair) {
+    const uint32_t* b = pair ? h_aff : sig_aff;
+    return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
+  };
+  auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k); };
+#if CESS_MILLER_MODE == 3
+  __shared__ uint4 T[18][256];
+  const GlobF12 fa{fout, stride, i}, fb{pp, stride, i};
+  if (miller_loop2_pp(fa, fb, LdsF12{T, threadIdx.x}, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src))
+    copy12(fa, fb);
+#else
+  miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src);
 #if CESS_MILLER_MODE == 2
 #pragma unroll 1
   for (int k = 0; k < 3; k++) f.hi.st(k, f.lo.ld(k));
 #elif CESS_MILLER_MODE == 0
   copy12(GlobF12{fout, stride, i}, f);
+#endif
 #endif
 }

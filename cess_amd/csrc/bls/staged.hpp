@@ -339,14 +339,32 @@ CESS_HD void inv12(const S& f) {
 // once in the code object; the hard part's five cyclotomic exponentiations by
 // x are spelled out as square runs and multiplies by the base.
 // ---------------------------------------------------------------------------
-enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_END };
-enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6, SL_N };
+enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_CHAIN, FE_END };
+enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6,
+                        SL_X0, SL_X1, SL_X2, SL_X3, SL_X4, SL_X5, SL_N };
 
-// a^x (x = -0xd201000000010000) for a in slot s: bits below the top one are
-// 62, 60, 57, 48, 16 -> square runs 1, 2, 3, 9, 32, 16
+// a^x (x = -0xd201000000010000) for a in slot s.
+// Default: bits below the top one are 62, 60, 57, 48, 16 -> Granger-Scott
+// square runs 1, 2, 3, 9, 32, 16 interleaved with multiplies by the base.
+// CESS_FE_KARABINA=1: |x| has bits 63, 62, 60, 57, 48, 16, so a^|x| = a^(2^63)
+// a^(2^62) a^(2^60) a^(2^57) a^(2^48) a^(2^16); FE_CHAIN s runs the 63 squarings
+// in compressed form and leaves the six powers, decompressed with one
+// inversion, in slots X5..X0, and the multiplies follow.  Bit-exact (host
+// emulation and GPU tests), but measured slower on MI355X (k_final 222 ms vs
+// 208 ms per 1 M: 2.2 KB/lane of scratch in the register-resident compressed
+// loop), so it is off.
+#ifndef CESS_FE_KARABINA
+#define CESS_FE_KARABINA 0
+#endif
+#if CESS_FE_KARABINA
+#define CESS_FE_CYCEXP(s) \
+  {FE_CHAIN, s}, {FE_LOAD, SL_X5}, {FE_MUL, SL_X4}, {FE_MUL, SL_X3}, {FE_MUL, SL_X2}, {FE_MUL, SL_X1}, \
+      {FE_MUL, SL_X0}, {FE_CONJ, 0}
+#else
 #define CESS_FE_CYCEXP(s) \
   {FE_LOAD, s}, {FE_SQN, 1}, {FE_MUL, s}, {FE_SQN, 2}, {FE_MUL, s}, {FE_SQN, 3}, {FE_MUL, s}, {FE_SQN, 9}, \
       {FE_MUL, s}, {FE_SQN, 32}, {FE_MUL, s}, {FE_SQN, 16}, {FE_CONJ, 0}
+#endif
 
 // easy part: m = f^((p^6 - 1)(p^2 + 1)); hard part as in pairing.hpp
 // final_exponentiation (t2 = m).  SL_T0 doubles as scratch in the easy part.
@@ -415,6 +433,77 @@ CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
   acc.st(5, z5);
 }
 
+// FE_CHAIN: the powers a^(2^k), k = 16, 48, 57, 60, 62, 63, of the cyclotomic
+// element a (store `base`) into the stores X(0..5).  The 63 squarings run on
+// (z2, z3, z4, z5) in registers (cyc_sqr_compressed); z1 of the six powers is
+// recovered with ONE Fp2 inversion (Montgomery's simultaneous-inversion trick:
+// prefix products of the denominators parked in the z0 words, numerators in the
+// z1 words), then z0.  A lane whose denominator is zero (z2 = z3 = 0, e.g. a = 1
+// from an identity pair) recomputes its chain with full Granger-Scott squarings
+// (divergent, rare).  Costs 63 x 4 Fp2 products + ~0.25k multiplies, against
+// 63 x 9 Fp2 squarings.
+template <class B, class XFn, class P>
+CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
+  {
+    fp2 z2 = base.ld(3), z3 = base.ld(2), z4 = base.ld(1), z5 = base.ld(5);
+    int k = 0;
+#pragma unroll 1
+    for (int j = 0; j < 6; j++) {
+      const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+#pragma unroll 1
+      for (; k < stop; k++) {
+        cyc_sqr_compressed(z2, z3, z4, z5);
+        CESS_MEMBAR();
+      }
+      const auto x = X(j);
+      x.st(3, z2);
+      x.st(2, z3);
+      x.st(1, z4);
+      x.st(5, z5);
+      CESS_MEMBAR();
+    }
+  }
+  bool degen = false;
+  fp2 prod = fp2_one();
+#pragma unroll 1
+  for (int j = 0; j < 6; j++) {
+    const auto x = X(j);
+    fp2 num, den;
+    cyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
+    const bool z = is_zero(den);
+    degen = degen || z;
+    x.st(4, num);
+    x.st(0, prod);   // product of the denominators before j
+    prod = mul(prod, select(z, fp2_one(), den));
+    CESS_MEMBAR();
+  }
+  fp2 iv = inv(prod);
+#pragma unroll 1
+  for (int j = 5; j >= 0; j--) {
+    const auto x = X(j);
+    fp2 num, den;
+    const fp2 z2 = x.ld(3), z3 = x.ld(2), z4 = x.ld(1), z5 = x.ld(5);
+    cyc_z1_frac(z2, z3, z4, z5, num, den);
+    const fp2 ivj = mul(iv, x.ld(0));   // 1 / den_j
+    iv = mul(iv, select(is_zero(den), fp2_one(), den));
+    const fp2 z1 = mul(x.ld(4), ivj);
+    x.st(4, z1);
+    x.st(0, cyc_z0(z1, z2, z3, z4, z5));
+    CESS_MEMBAR();
+  }
+  if (degen) {   // full squarings on X(5) as the running power
+    const auto w = X(5);
+    copy12(w, base);
+#pragma unroll 1
+    for (int j = 0; j < 5; j++) {
+      const int run = j == 0 ? 16 : j == 1 ? 32 : j == 2 ? 9 : j == 3 ? 3 : 2;
+      cyc_square_run_parked(w, pk, run);
+      copy12(X(j), w);
+    }
+    cyc_square_run_parked(w, pk, 1);
+  }
+}
+
 // Run the program.  The accumulator alternates between the stores acc0 and
 // acc1: FE_MUL writes the product of the current one and a slot into the other
 // (mul12_stream, with the parking store `pk` as its Fp6 temporary); every other
@@ -459,6 +548,9 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
       case FE_CONJ: conj12(acc); break;
       case FE_FROB: frob12(acc, arg); break;
       case FE_INV: inv12(acc); break;
+#if CESS_FE_KARABINA
+      case FE_CHAIN: cyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }, pk); break;
+#endif
       default: break;
     }
   }

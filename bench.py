@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=40960, help="records for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
-    ap.add_argument("--mode", choices=["persig", "rlc", "adversarial"], default="persig",
+    ap.add_argument("--mode", choices=["persig", "rlc", "adversarial", "keyed"], default="persig",
                     help="persig: BASELINE config[1] (default); rlc: config[3] shape (few keys, RLC batch "
                          "mode + Gt-partial combine); adversarial: config[4] shape (1%% invalid mix, exact codes)")
     ap.add_argument("--keys", type=int, default=16, help="distinct keys (rlc mode)")
@@ -83,6 +83,28 @@ def make_dataset(ctx, n, seed, forged_frac):
         sign_msgs[idx, 0] ^= 0xFF      # valid signature over a different message
     sigs = ctx.sign(sks, [bytes(r) for r in sign_msgs])
     return b"".join(sigs), b"".join(pks), msgs.tobytes(), forged
+
+
+def make_keyed_dataset(ctx, n, k, seed, forged_frac):
+    """Few-keys workload (BASELINE config[3]'s shape, per-signature verdicts):
+    k distinct keys, signature i by key i % k over its own 32-byte message."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    sk = rng.integers(0, 256, size=(k, 32), dtype=np.uint8)
+    sk[:, 0] &= 0x3F
+    sk[:, 31] |= 1
+    sks = [bytes(r) for r in sk]
+    pks = ctx.public_keys(sks)
+    who = (np.arange(n) % k).astype(np.uint32)
+    msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sign_msgs = msgs.copy()
+    forged = np.zeros(n, dtype=bool)
+    if forged_frac > 0:
+        idx = rng.choice(n, size=max(1, int(n * forged_frac)), replace=False)
+        forged[idx] = True
+        sign_msgs[idx, 0] ^= 0xFF
+    sigs = ctx.sign([sks[w] for w in who], [bytes(r) for r in sign_msgs])
+    return b"".join(sigs), pks, who, msgs.tobytes(), forged
 
 
 def inject_adversarial(S, P, M, n, seed, frac=0.01):
@@ -228,14 +250,22 @@ def main():
         return
     n = args.n
     ctx = bls.Context(device=local, max_batch=n, profile=True)
-    S, P, M, forged = make_dataset(ctx, n, seed=(0x00C0FFEE, rank), forged_frac=args.forged_frac)
     import numpy as np
+    keyed = args.mode == "keyed"
+    if keyed:
+        S, key_list, who, M, forged = make_keyed_dataset(ctx, n, args.keys, seed=(0x00C0FFEE, rank),
+                                                         forged_frac=args.forged_frac)
+        P = b"".join(key_list[w] for w in who)     # expanded records, for the CPU baseline only
+        assert ctx.load_keys(key_list) == bytes(len(key_list))
+        d_idx = torch.from_numpy(who.astype(np.int32)).to(dev)
+    else:
+        S, P, M, forged = make_dataset(ctx, n, seed=(0x00C0FFEE, rank), forged_frac=args.forged_frac)
     expect = np.where(forged, 5, 0).astype(np.uint8)
     n_adv_kinds = 0
     if args.mode == "adversarial":
         S, P, M, expect, n_adv_kinds = inject_adversarial(S, P, M, n, seed=(0xADD, rank))
     d_sig = torch.frombuffer(bytearray(S), dtype=torch.uint8).to(dev)
-    d_pk = torch.frombuffer(bytearray(P), dtype=torch.uint8).to(dev)
+    d_pk = None if keyed else torch.frombuffer(bytearray(P), dtype=torch.uint8).to(dev)
     d_msg = torch.frombuffer(bytearray(M), dtype=torch.uint8).to(dev)
     d_off = (torch.arange(n + 1, dtype=torch.int64) * 32).to(dev)
     d_codes = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -243,8 +273,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        ctx.verify_device(n, d_sig.data_ptr(), d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
-                          d_codes.data_ptr(), d_bitmap.data_ptr(), stream.cuda_stream)
+        if keyed:
+            ctx.verify_keyed_device(n, d_sig.data_ptr(), d_idx.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
+                                    d_codes.data_ptr(), d_bitmap.data_ptr(), stream.cuda_stream)
+        else:
+            ctx.verify_device(n, d_sig.data_ptr(), d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
+                              d_codes.data_ptr(), d_bitmap.data_ptr(), stream.cuda_stream)
         return gather_bitmap(d_bitmap, n * world, world) if world > 1 else d_bitmap
 
     for _ in range(args.warmup):
@@ -262,6 +296,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stages = ctx.stage_times(reset=True)   # HIP events on the launch stream, timed region only
+    if keyed:   # the keyed pipeline runs k_merge_pk in k_decode_pk's slot and has no per-signature prepare
+        stages["k_merge_pk"] = stages.pop("k_decode_pk")
+        stages.pop("k_prepare", None)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -280,6 +317,9 @@ def main():
         value = total / elapsed
         oc = load_opcount()
         per = oc["per_stage"]
+        whole_mads = oc["algorithmic_mads_per_sig"]
+        if keyed:   # per-key decode + prepare are done once per key, outside the per-signature work
+            whole_mads -= sum((per[k]["mul"] + per[k]["sqr"]) * ALG_MADS_PER_FP_MUL for k in ("k_decode_pk", "k_prepare"))
         dom = max(stages, key=lambda k: stages[k])
         dom_ms = stages[dom] / args.steps                  # per launch (one launch per step, chunk = n)
         alg = (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL * n
@@ -309,6 +349,9 @@ def main():
             "data": "synthetic: random distinct keys + 32-byte messages, keys/sigs generated on GPU",
             "config": {"workload": (f"BASELINE config[1]: {n} independent sigs per GPU, distinct keys, "
                                     f"per-sig 2-pairing verify" if args.mode == "persig" else
+                                    f"BASELINE config[3] shape, per-signature verdicts: {n} sigs per GPU over "
+                                    f"{args.keys} keys, key decode + G2Prepared once per key (keyed batch)"
+                                    if keyed else
                                     f"BASELINE config[4] shape: {n} sigs per GPU, 1% invalid (half forged, half "
                                     f"{n_adv_kinds} kinds of malformed/non-subgroup/identity records), exact codes")
                                    + (", RCCL allgather of verdict bitmap" if world > 1 else ""),
@@ -321,7 +364,7 @@ def main():
                          "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
                          "frac": achieved / PEAK_MADS, "traffic": traffic,
                          "alg_mads_per_sig": (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL,
-                         "whole_path_frac": oc["algorithmic_mads_per_sig"] * value / world / PEAK_MADS},
+                         "whole_path_frac": whole_mads * value / world / PEAK_MADS},
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

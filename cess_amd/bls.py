@@ -39,6 +39,7 @@ EXPORTS = (
     "cess_bls_sign_batch", "cess_bls_hash_to_g1_batch", "cess_bls_gt_batch", "cess_bls_stage_times",
     "cess_bls_status_string", "cess_bls_version",
     "cess_bls_verify_batch_rlc", "cess_bls_rlc_begin", "cess_bls_gt_product_is_one", "cess_bls_rlc_finish",
+    "cess_bls_keys_load", "cess_bls_verify_batch_keyed", "cess_bls_verify_batch_keyed_device",
 )
 
 
@@ -78,6 +79,10 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_verify_batch.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u64p]
         lib.cess_bls_verify_batch_var.argtypes = [vp, sz, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p]
         lib.cess_bls_verify_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
+        lib.cess_bls_keys_load.argtypes = [vp, sz, _u8p, _u8p]
+        lib.cess_bls_verify_batch_keyed.argtypes = [vp, sz, _u8p, ctypes.POINTER(ctypes.c_uint32), _u8p, _u64p,
+                                                    _u8p, _u64p]
+        lib.cess_bls_verify_batch_keyed_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
         lib.cess_bls_public_key_batch.argtypes = [vp, sz, _u8p, _u8p]
         lib.cess_bls_sign_batch.argtypes = [vp, sz, _u8p, _u8p, _u64p, _u8p]
         lib.cess_bls_hash_to_g1_batch.argtypes = [vp, sz, _u8p, _u64p, _u8p]
@@ -194,6 +199,34 @@ class Context:
         """Device-resident batch (HBM pointers as ints); enqueued on `stream`, not synchronised."""
         self._chk(self._lib.cess_bls_verify_batch_device(self._h, n, d_sigs, d_pks, d_msgs, d_offs, d_codes,
                                                          d_bitmap, stream or None))
+
+    # --- distinct-key table (per-key decode + G2Prepared done once) -------
+    def load_keys(self, keys: Sequence[bytes]) -> bytes:
+        """Decode and prepare each distinct 96-byte key once (PublicKey::deserialize,
+        src/lib.rs:68-82, and G2Prepared::from, :88); returns the per-key codes
+        (0, or 4 = PK_POINT).  Replaces any previously loaded table."""
+        k = len(keys)
+        assert all(len(bytes(x)) == 96 for x in keys)
+        kc = (ctypes.c_uint8 * max(k, 1))()
+        self._chk(self._lib.cess_bls_keys_load(self._h, k, _buf(b"".join(bytes(x) for x in keys)), kc))
+        return bytes(kc)[:k]
+
+    def verify_keyed(self, sigs: bytes, key_idx: Sequence[int], msgs: bytes, msg_offsets) -> Tuple[bytes, list]:
+        """Per-signature verdicts where signature i is checked against loaded key
+        key_idx[i]; same codes as the per-record path on the expanded records."""
+        n = len(sigs) // 48
+        assert len(sigs) == 48 * n and len(key_idx) == n
+        idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        offs = (ctypes.c_uint64 * (n + 1))(*msg_offsets)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        self._chk(self._lib.cess_bls_verify_batch_keyed(self._h, n, _buf(sigs), idx, _buf(msgs), offs, codes, bitmap))
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64]
+
+    def verify_keyed_device(self, n, d_sigs, d_key_idx, d_msgs, d_offs, d_codes, d_bitmap, stream=0):
+        """Device-resident keyed batch (HBM pointers as ints); not synchronised."""
+        self._chk(self._lib.cess_bls_verify_batch_keyed_device(self._h, n, d_sigs, d_key_idx, d_msgs, d_offs,
+                                                               d_codes, d_bitmap, stream or None))
 
     # --- RLC batch mode (random linear combination + bisection) ----------
     def rlc_begin(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: bytes) -> bytes:

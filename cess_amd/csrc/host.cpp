@@ -20,7 +20,8 @@ __global__ void k_decode_pk(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, 
 __global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*, uint32_t*, uint64_t);
 __global__ void k_prepare(uint64_t, const uint32_t*, uint4*, uint64_t);
 __global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                         const uint4*, uint4*, uint4*, uint64_t);
+                         const uint4*, uint4*, uint4*, uint64_t, const uint32_t*, uint64_t);
+__global__ void k_merge_pk(uint64_t, const uint32_t*, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*);
 __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
@@ -99,6 +100,9 @@ struct cess_bls_ctx {
   hipEvent_t ev[ST_N + 1] = {};
   double stage_ms[ST_N] = {};
   RlcState* rlc = nullptr;
+  // distinct-key table (cess_bls_keys_load): decoded keys + G2Prepared rows, stride = nkeys
+  uint32_t nkeys = 0;
+  DevBuf key_in, key_code, key_inf, key_aff, key_coeffs, in_idx;
 };
 
 #define HIPCHK(x)                          \
@@ -232,7 +236,7 @@ static int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* 
   hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
                      (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
                      (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)c->coeffs.as<uint4>(),
-                     c->fval.as<uint4>(), c->fe_slots.as<uint4>(), st);
+                     c->fval.as<uint4>(), c->fe_slots.as<uint4>(), st, (const uint32_t*)nullptr, st);
   if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
   hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,
                      gt, st);
@@ -359,6 +363,128 @@ extern "C" int cess_bls_verify_batch_device(cess_bls_ctx* c, size_t n, const uin
       r = collect_profile(c, s);
       if (r) return r;
     }
+  }
+  return CESS_BLS_OK;
+}
+
+// distinct-key table ---------------------------------------------------------
+// Per-key work of PublicKey::deserialize (src/lib.rs:68-82) and
+// G2Prepared::from (:88) done once per distinct key (SURVEY §8(a) A5/A11:
+// "cacheable per distinct pk"); the keyed batches then index the table.
+extern "C" int cess_bls_keys_load(cess_bls_ctx* c, size_t k, const uint8_t* pks, uint8_t* key_codes_out) {
+  if (!c || (k && !pks) || k > 0xffffffffull) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  c->nkeys = 0;
+  if (k == 0) return CESS_BLS_OK;
+  int r = c->key_in.ensure(k * 96) | c->key_code.ensure(k) | c->key_inf.ensure(k) |
+          c->key_aff.ensure(k * CESS_W_G2 * 4) | c->key_coeffs.ensure(k * (uint64_t)CESS_W_COEFFS * 4);
+  if (r) return CESS_BLS_E_OOM;
+  HIPCHK(hipMemcpyAsync(c->key_in.p, pks, k * 96, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(c->key_code.p, 0, k, s));
+  HIPCHK(hipMemsetAsync(c->key_inf.p, 0, k, s));
+  hipLaunchKernelGGL(k_decode_pk, dim3(grid_for(k)), dim3(kBlock), 0, s, (uint64_t)k, c->key_in.as<uint8_t>(),
+                     (const uint8_t*)nullptr, c->key_code.as<uint8_t>(), c->key_inf.as<uint8_t>(),
+                     c->key_aff.as<uint32_t>(), (uint64_t)k);
+  hipLaunchKernelGGL(k_prepare, dim3(grid_for(k)), dim3(kBlock), 0, s, (uint64_t)k,
+                     (const uint32_t*)c->key_aff.as<uint32_t>(), c->key_coeffs.as<uint4>(), (uint64_t)k);
+  HIPCHK(hipGetLastError());
+  if (key_codes_out) HIPCHK(hipMemcpyAsync(key_codes_out, c->key_code.p, k, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  c->nkeys = (uint32_t)k;
+  return CESS_BLS_OK;
+}
+
+// One chunk of a keyed batch: sig decode, key verdicts from the table, hash,
+// Miller loop over the table's coefficient rows, final exponentiation.
+static int run_chunk_keyed(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* sigs, const uint32_t* idx,
+                           const uint8_t* msgs, const uint64_t* offs, uint8_t* codes, uint64_t* bitmap) {
+  const uint64_t st = c->cap;
+  const bool prof = (c->flags & CESS_BLS_F_PROFILE) != 0;
+  const unsigned g = grid_for(n);
+  uint8_t* inf = c->inf.as<uint8_t>();
+  if (prof) HIPCHK(hipEventRecord(c->ev[0], s));
+  hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, n, sigs, (const uint8_t*)nullptr, codes, inf,
+                     c->sig_aff.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[1], s));
+  hipLaunchKernelGGL(k_merge_pk, dim3(g), dim3(kBlock), 0, s, n, idx, (const uint8_t*)c->key_code.as<uint8_t>(),
+                     (const uint8_t*)c->key_inf.as<uint8_t>(), codes, inf);
+  if (prof) HIPCHK(hipEventRecord(c->ev[2], s));
+  hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes, c->h_aff.as<uint32_t>(), st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[3], s));
+  if (prof) HIPCHK(hipEventRecord(c->ev[4], s));
+  hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
+                     (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)c->key_coeffs.as<uint4>(),
+                     c->fval.as<uint4>(), c->fe_slots.as<uint4>(), st, idx, (uint64_t)c->nkeys);
+  if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
+  hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,
+                     (uint8_t*)nullptr, st);
+  if (prof) HIPCHK(hipEventRecord(c->ev[6], s));
+  HIPCHK(hipGetLastError());
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_verify_batch_keyed_device(cess_bls_ctx* c, size_t n, const uint8_t* d_sigs,
+                                                  const uint32_t* d_key_idx, const uint8_t* d_msgs,
+                                                  const uint64_t* d_offs, uint8_t* d_codes, uint64_t* d_bitmap,
+                                                  void* stream) {
+  if (!c || !d_sigs || !d_key_idx || !d_offs || !d_codes) return CESS_BLS_E_INVALID_ARG;
+  if (n == 0) return CESS_BLS_OK;
+  if (c->nkeys == 0) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  for (size_t off = 0; off < n; off += c->cap) {
+    uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    int r = run_chunk_keyed(c, s, m, d_sigs + 48 * off, d_key_idx + off, d_msgs, d_offs + off, d_codes + off,
+                            d_bitmap ? d_bitmap + off / 64 : c->bitmap.as<uint64_t>());
+    if (r) return r;
+    r = collect_profile(c, s);
+    if (r) return r;
+  }
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_verify_batch_keyed(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint32_t* key_idx,
+                                           const uint8_t* msgs, const uint64_t* offs, uint8_t* codes_out,
+                                           uint64_t* bitmap_out) {
+  if (!c) return CESS_BLS_E_INVALID_ARG;
+  if (n == 0) return CESS_BLS_OK;
+  if (!sigs || !key_idx || !offs || (!msgs && offs[n] != offs[0])) return CESS_BLS_E_INVALID_ARG;
+  if (c->nkeys == 0) return CESS_BLS_E_INVALID_ARG;
+  // an out-of-range key index would read past the table: reject it on the host
+  for (size_t i = 0; i < n; i++)
+    if (key_idx[i] >= c->nkeys) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  std::vector<uint64_t> rebased, words;
+  for (size_t off = 0; off < n; off += c->cap) {
+    uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    uint64_t mb0 = offs[off], mb1 = offs[off + m];
+    if (mb1 < mb0) return CESS_BLS_E_INVALID_ARG;
+    rebased.resize(m + 1);
+    for (uint64_t j = 0; j <= m; j++) {
+      if (j && offs[off + j] < offs[off + j - 1]) return CESS_BLS_E_INVALID_ARG;
+      rebased[j] = offs[off + j] - mb0;
+    }
+    int r = c->in_sigs.ensure(m * 48) | c->in_idx.ensure(m * 4) | c->in_msgs.ensure(std::max<uint64_t>(mb1 - mb0, 1)) |
+            c->in_offs.ensure((m + 1) * 8);
+    if (r) return CESS_BLS_E_OOM;
+    HIPCHK(hipMemcpyAsync(c->in_sigs.p, sigs + 48 * off, m * 48, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_idx.p, key_idx + off, m * 4, hipMemcpyHostToDevice, s));
+    if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+    r = run_chunk_keyed(c, s, m, c->in_sigs.as<uint8_t>(), c->in_idx.as<uint32_t>(), c->in_msgs.as<uint8_t>(),
+                        c->in_offs.as<uint64_t>(), c->code.as<uint8_t>(), c->bitmap.as<uint64_t>());
+    if (r) return r;
+    if (codes_out) HIPCHK(hipMemcpyAsync(codes_out + off, c->code.p, m, hipMemcpyDeviceToHost, s));
+    uint64_t nw = (m + 63) / 64;
+    words.resize(nw);
+    HIPCHK(hipMemcpyAsync(words.data(), c->bitmap.p, nw * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (bitmap_out) memcpy(bitmap_out + off / 64, words.data(), nw * 8);
+    r = collect_profile(c, s);
+    if (r) return r;
   }
   return CESS_BLS_OK;
 }
@@ -506,7 +632,7 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
                      (const uint8_t*)R.rec_code.as<uint8_t>(), (const uint8_t*)R.rec_inf.as<uint8_t>(),
                      (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
                      (const uint32_t*)c->neg_g2.as<uint32_t>(), coeffs, R.rec_f.as<uint4>(), R.rec_f2.as<uint4>(),
-                     (uint64_t)M);
+                     (uint64_t)M, (const uint32_t*)nullptr, (uint64_t)M);
   hipLaunchKernelGGL(k_fp12_prod_multi, dim3((NR + 63) / 64), dim3(64), 0, s, NR, K, (const uint4*)R.rec_f.as<uint4>(),
                      R.acc.as<uint4>());
   HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));

@@ -69,3 +69,19 @@ __global__ CESS_LB void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
   code[i] = c;
   inf[i] = f;
 }
+
+// keyed batch (cess_bls_verify_batch_keyed*): per-signature key verdicts taken
+// from the distinct-key table in the reference's precedence -- a bad signature
+// code stands, else the key's code, else the key's identity flag
+// (src/lib.rs:244-245)
+__global__ CESS_LB void k_merge_pk(uint64_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ key_code,
+                                   const uint8_t* __restrict__ key_inf, uint8_t* __restrict__ code,
+                                   uint8_t* __restrict__ inf) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (code[i] != 0) return;
+  const uint32_t j = idx[i];
+  const uint8_t kc = key_code[j];
+  if (kc != 0) code[i] = kc;
+  else inf[i] |= key_inf[j] & INF_PK;
+}

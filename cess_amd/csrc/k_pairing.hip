@@ -55,10 +55,14 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
                                      const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
                                      const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
                                      const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
-                                     uint4* __restrict__ pp, uint64_t stride) {
+                                     uint4* __restrict__ pp, uint64_t stride,
+                                     const uint32_t* __restrict__ cidx, uint64_t cstride) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (code[i] != 0) return;
+  // coefficient row: the lane's own (per-signature prepare) or, for the keyed
+  // batch, its key's row in the distinct-key table (cstride = table stride)
+  const uint32_t cj = cidx ? cidx[i] : i;
   uint8_t fl = inf[i];
 #if CESS_MILLER_MODE == 3
 #elif CESS_MILLER_MODE == 1
@@ -76,7 +80,7 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
     const uint32_t* b = pair ? h_aff : sig_aff;
     return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
   };
-  auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, stride, i, k) : ld_coeff_uniform(neg_g2, k); };
+  auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, cstride, cj, k) : ld_coeff_uniform(neg_g2, k); };
 #if CESS_MILLER_MODE == 3
   __shared__ uint4 T[18][256];
   const GlobF12 fa{fout, stride, i}, fb{pp, stride, i};

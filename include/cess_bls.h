@@ -95,6 +95,29 @@ int cess_bls_verify_batch_device(cess_bls_ctx* ctx, size_t n, const uint8_t* d_s
                                  const uint8_t* d_msgs, const uint64_t* d_msg_offsets, uint8_t* d_codes,
                                  uint64_t* d_bitmap, void* stream);
 
+/* Distinct-key table (key decode and G2Prepared are
+ * "cacheable per distinct pk"; §8(f) rank 3).  Decodes k 96-byte keys
+ * (PublicKey::deserialize, src/lib.rs:68-82) and prepares their line
+ * coefficients (G2Prepared::from, src/lib.rs:88) once, on the device;
+ * key_codes_out (k bytes, may be NULL) receives 0 or CESS_BLS_PK_POINT.
+ * Replaces the context's previous table.  Host buffer. */
+int cess_bls_keys_load(cess_bls_ctx* ctx, size_t k, const uint8_t* pks, uint8_t* key_codes_out);
+
+/* Keyed batch: signature i (48 B) over message i is verified against loaded
+ * key key_idx[i] (< k, checked; else CESS_BLS_E_INVALID_ARG).  Codes and
+ * bitmap equal cess_bls_verify_batch on the expanded records (same
+ * precedence: signature first, src/lib.rs:244-245).  Host buffers. */
+int cess_bls_verify_batch_keyed(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint32_t* key_idx,
+                                const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* codes_out,
+                                uint64_t* bitmap_out);
+
+/* Device-resident keyed batch (as cess_bls_verify_batch_device; the caller
+ * guarantees every d_key_idx[i] < k). */
+int cess_bls_verify_batch_keyed_device(cess_bls_ctx* ctx, size_t n, const uint8_t* d_sigs,
+                                       const uint32_t* d_key_idx, const uint8_t* d_msgs,
+                                       const uint64_t* d_msg_offsets, uint8_t* d_codes, uint64_t* d_bitmap,
+                                       void* stream);
+
 /* PrivateKey::public_key (src/lib.rs:226-228) for n 32-byte big-endian secret
  * keys (each must be < r, as PrivateKey::deserialize enforces at :208-223);
  * pks_out: n * 96 bytes. */

@@ -134,9 +134,7 @@ static int alloc_stage(cess_bls_ctx* c) {
   r |= c->code.ensure(n);
   r |= c->inf.ensure(n);
   r |= c->sig_aff.ensure(n * CESS_W_G1 * 4);
-  r |= c->pk_aff.ensure(n * CESS_W_G2 * 4);
   r |= c->h_aff.ensure(n * CESS_W_G1 * 4);
-  r |= c->coeffs.ensure(n * (uint64_t)CESS_W_COEFFS * 4);
   r |= c->fval.ensure(n * CESS_W_FP12 * 4);
   r |= c->fe_slots.ensure(n * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
   r |= c->bitmap.ensure((n / 64 + 1) * 8);
@@ -220,6 +218,9 @@ static int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* 
                      const uint8_t* msgs, const uint64_t* offs, const uint8_t* pre, uint8_t* codes, uint64_t* bitmap,
                      uint8_t* gt) {
   const uint64_t st = c->cap;
+  // per-record key buffers (19.6 KB of line coefficients per signature) are
+  // allocated on first use: keyed batches never touch them
+  if (c->pk_aff.ensure(st * CESS_W_G2 * 4) | c->coeffs.ensure(st * (uint64_t)CESS_W_COEFFS * 4)) return CESS_BLS_E_OOM;
   const bool prof = (c->flags & CESS_BLS_F_PROFILE) != 0;
   const unsigned g = grid_for(n);
   uint8_t* inf = c->inf.as<uint8_t>();

@@ -475,10 +475,35 @@ class Verdicts:
         return bool((self.bitmap[i >> 6] >> (i & 63)) & 1)
 
 
-def verify_batch(records: Iterable[Tuple[bytes, bytes, bytes]], ctx: Optional[Context] = None) -> Verdicts:
-    """New batch entry point: records of (sig, msg, key) -> Verdicts."""
+def verify_batch(records: Iterable[Tuple[bytes, bytes, bytes]], ctx: Optional[Context] = None,
+                 dedup_keys: bool = True) -> Verdicts:
+    """New batch entry point: records of (sig, msg, key) -> Verdicts.
+
+    With dedup_keys, a fixed-size batch whose records share few keys (at most
+    one distinct key per 8 records, e.g. TEE-signed audit verdicts) runs the
+    keyed path: each distinct key is decoded and prepared once
+    (cess_bls_keys_load, replacing the context's key table).  Codes are the
+    same as the per-record path (tests/test_gpu_keyed.py)."""
     records = list(records)
-    codes = (ctx or default_context()).verify_codes(records)
+    ctx = ctx or default_context()
+    n = len(records)
+    codes = None
+    if dedup_keys and n >= 256 and all(len(r[0]) == 48 and len(r[2]) == 96 for r in records):
+        kid = {}
+        for r in records:
+            kid.setdefault(bytes(r[2]), len(kid))
+            if 8 * len(kid) > n:
+                break
+        if 8 * len(kid) <= n:
+            ctx.load_keys(list(kid))
+            msgs = [bytes(r[1]) for r in records]
+            offs = [0]
+            for m in msgs:
+                offs.append(offs[-1] + len(m))
+            codes, _ = ctx.verify_keyed(b"".join(bytes(r[0]) for r in records), [kid[bytes(r[2])] for r in records],
+                                        b"".join(msgs), offs)
+    if codes is None:
+        codes = ctx.verify_codes(records)
     words = [0] * ((len(records) + 63) // 64)
     for i, c in enumerate(codes):
         if c == CODE_OK:

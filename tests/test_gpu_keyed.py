@@ -70,3 +70,16 @@ def test_keyed_rejects_bad_index(ctx):
     ctx.load_keys([bytes.fromhex("c0") + bytes(95)])
     with pytest.raises(bls.BlsInfraError):
         ctx.verify_keyed(bytes(48), [1], b"", [0, 0])
+
+
+def test_verify_batch_dedups_keys(ctx, vectors):
+    """The Python mirror's verify_batch routes few-key batches through the key
+    table; verdicts equal the per-record path, golden bad keys included."""
+    from cess_amd import bls
+    cases = _fixed_cases(vectors)
+    recs = [(bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])) for c in cases]
+    recs = (recs * (1 + 2048 // max(len(recs), 1)))[:2048]
+    assert 8 * len({r[2] for r in recs}) <= len(recs)
+    v = bls.verify_batch(recs, ctx=ctx)
+    ref = bls.verify_batch(recs, ctx=ctx, dedup_keys=False)
+    assert v.codes == ref.codes and v.bitmap == ref.bitmap

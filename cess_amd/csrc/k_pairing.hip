@@ -1,22 +1,12 @@
 // CDNA4 (gfx950) kernels for batch BLS12-381 verification — one lane = one signature.
 // Stage outputs live in HBM in limb-major SoA layout (soa.hpp).
-// k_prepare        : pk -> 68 line-coefficient triples (G2Prepared::from, src/lib.rs:88, A11)
-//                    (also builds the G2PREPARED_NEG_G table once per context, src/lib.rs:19-21, A10)
+// (k_prepare lives in k_prepare.hip: it is compiled with the default scheduler)
 // k_miller         : (sig,-G2),(H,pk) -> Miller-loop value (multi_miller_loop, src/lib.rs:90-93, A12)
 #include <hip/hip_runtime.h>
 #include "soa.hpp"
 
 using namespace bls;
 using namespace cess;
-
-__global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_aff,
-                                  uint4* __restrict__ coeffs, uint64_t stride) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  fp2 qx = ld_fp2(pk_aff, stride, i);
-  fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
-  g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); });
-}
 
 // Miller accumulator placement (CESS_MILLER_MODE):
 //   0: an LDS image (144 dwords x 256 lanes = 144 KiB, one wave per SIMD);

@@ -1,25 +1,40 @@
 """Benchmark: verified BLS12-381 signatures/s on MI355X (BASELINE.json metric).
 
-Workload (N=1): BASELINE config[1] — 1,048,576 independent signatures with
-distinct random keys over 32-byte messages, per-signature two-pairing verify,
-inputs resident in HBM.  N>1 (torch.distributed.run, one process per GPU):
-weak scaling, each rank verifies its own 1M-signature shard, then the verdict
-bitmap words are all-gathered over RCCL (xGMI) so every rank holds the full
-batch bitmap (BASELINE config[2] shape).
+Workloads (one process per GPU):
+  N = 1 : BASELINE config[1] -- 1,048,576 independent signatures with distinct
+          random keys over 32-byte messages, per-signature two-pairing verify.
+  N > 1 : BASELINE config[2] shape -- 2,097,152 signatures per GPU (16 M at
+          N = 8) sharded by index; each rank verifies its shard and the verdict
+          bitmap words (and code bytes) are all-gathered over RCCL (xGMI) INSIDE
+          the library (cess_bls_verify_batch_sharded_device), so every rank
+          holds the whole batch's verdicts.  Weak scaling: fixed work per GPU.
 
-A "step" = one verify_batch over the whole shard + the bitmap all-gather.
-Keys/signatures are generated on the GPU with the library's own keygen/sign
-kernels (untimed); a sample is checked against the CPU oracle in the tests.
+A "step" = one verify_batch over the shard (inputs resident in HBM) + the
+all-gather.  Keys/signatures are generated on the GPU with the library's own
+keygen/sign kernels (untimed); their parity with the CPU oracle is pinned by the
+tests.
+
+Launch: `python bench.py --gpus N` with no WORLD_SIZE in the environment starts
+N ranks itself (torch.distributed.run, 127.0.0.1) from this parent, which never
+touches the GPU; under torchrun (the driver's form) each rank runs directly.
+
+Runtime provenance: libcess_bls.so is loaded BEFORE anything else can pull in a
+HIP runtime, and the data path never calls torch, so the kernels and RCCL are
+the /opt/rocm builds the tests use; the JSON line records the mapped
+libamdhip64 / librccl paths and the library's SHA-256, and `roofline.traffic`
+is taken only from a PMC profile of that same library build.
 
 Prints ONE JSON line on rank 0 (contract in the task brief), including
 `roofline` (dominant kernel vs the v_mad_u64_u32 peak) and `cpu_baseline`
-(the build's CPU path, tests/hostemu/cpu_verify.cpp, timed on the host cores on a
-bounded sample).
+(the build's CPU path, tests/hostemu/cpu_verify.cpp, on a bounded sample).
 """
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -30,24 +45,118 @@ sys.path.insert(0, ROOT)
 # profiles/r01_mad_peak.txt) x 2.4 GHz.
 PEAK_MADS = 256 * 64 * 2.4e9
 ALG_MADS_PER_FP_MUL = 288   # 12^2 (a*b) + 12^2 (m*p) 32x32-bit limb products
+N1_DEFAULT = 1 << 20        # config[1]
+NPER_MULTI = 1 << 21        # config[2]: 16 M over 8 GPUs
 
 
 def parse():
+    """Command-line flags; ranks started by launch() receive the parent's flags
+    through CESS_BENCH_ARGV (torch.distributed.run would otherwise try to
+    prefix-match flags such as --n against its own options)."""
+    argv = json.loads(os.environ["CESS_BENCH_ARGV"]) if "CESS_BENCH_ARGV" in os.environ else None
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU")
+    ap.add_argument("--n", type=int, default=None,
+                    help="signatures per GPU (default: 1,048,576 at N=1 = config[1]; 2,097,152 at N>1 = config[2])")
     ap.add_argument("--forged-frac", type=float, default=0.0)
     ap.add_argument("--cpu-sample", type=int, default=40960, help="records for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--mode", choices=["persig", "rlc", "adversarial", "keyed"], default="persig",
-                    help="persig: BASELINE config[1] (default); rlc: config[3] shape (few keys, RLC batch "
-                         "mode + Gt-partial combine); adversarial: config[4] shape (1%% invalid mix, exact codes)")
-    ap.add_argument("--keys", type=int, default=16, help="distinct keys (rlc mode)")
+                    help="persig: BASELINE config[1]/[2] (default); rlc: config[3] shape (few keys, RLC batch "
+                         "mode + Gt-partial all-gather); adversarial: config[4] shape (1%% invalid mix, exact codes); "
+                         "keyed: config[3] shape with per-signature verdicts")
+    ap.add_argument("--keys", type=int, default=16, help="distinct keys (rlc / keyed modes)")
     ap.add_argument("--forged-count", type=int, default=0, help="forgeries per rank (rlc mode)")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rendezvous/sharding only, no GPU (CPU test of the N>1 path)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher + rendezvous (no GPU in this process)
+# ---------------------------------------------------------------------------
+def launch(args) -> int:
+    """Start args.gpus ranks with torch.distributed.run and return its exit code.
+    This parent process makes no HIP call (it only imports the launcher)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+               CESS_BENCH_ARGV=json.dumps(sys.argv[1:]))
+    return subprocess.call(cmd, env=env)
+
+
+def rdv_dir() -> str:
+    """Per-job rendezvous directory: all ranks of one torchrun job share the
+    agent (parent) pid and the master port."""
+    key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    d = os.path.join(tempfile.gettempdir(), f"cess_bls_rdv_{key}")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def rdv_put(name: str, data: bytes):
+    d = rdv_dir()
+    tmp = os.path.join(d, f".{name}.{os.getpid()}")
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, os.path.join(d, name))
+
+
+def rdv_get(name: str, timeout: float = 300.0) -> bytes:
+    p = os.path.join(rdv_dir(), name)
+    t0 = time.time()
+    while not os.path.exists(p):
+        if time.time() - t0 > timeout:
+            raise TimeoutError(f"rendezvous: {p} never appeared")
+        time.sleep(0.05)
+    with open(p, "rb") as f:
+        return f.read()
+
+
+def rdv_cleanup(rank: int, world: int):
+    if rank == 0:
+        import shutil
+        shutil.rmtree(rdv_dir(), ignore_errors=True)
+
+
+def comm_setup(ctx, rank: int, world: int):
+    """ncclUniqueId from rank 0 to every rank (file rendezvous), then
+    ncclCommInitRank inside the library."""
+    from cess_amd import bls
+    if rank == 0:
+        rdv_put("comm_id", bls.comm_id())
+    cid = rdv_get("comm_id")
+    ctx.comm_init(world, rank, cid)
+    ctx.comm_barrier()
+    rdv_cleanup(rank, world)
+
+
+def runtime_provenance() -> dict:
+    maps = {}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.strip() else ""
+                for key in ("libamdhip64", "librccl", "libcess_bls"):
+                    if key in p and "/" in p:
+                        maps.setdefault(key, p)
+    except OSError:
+        pass
+    return maps
+
+
+def lib_sha256() -> str:
+    p = os.path.join(ROOT, "cess_amd", "lib", "libcess_bls.so")
+    with open(p, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
 def load_opcount():
@@ -55,17 +164,23 @@ def load_opcount():
         return json.load(f)
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC summary (profiles/*_pmc_traffic.json), if one exists."""
+def load_pmc_traffic(sha: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary
+    (profiles/*_pmc_traffic.json) measured on THIS library build (same
+    SHA-256); None when no profile of this build exists."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        return json.load(f)
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("lib_sha256") == sha:
+            d["_file"] = os.path.relpath(p, ROOT)
+            return d
+    return None
 
 
+# ---------------------------------------------------------------------------
+# synthetic datasets (generated on the GPU by the library's keygen/sign kernels)
+# ---------------------------------------------------------------------------
 def make_dataset(ctx, n, seed, forged_frac):
     import numpy as np
     rng = np.random.default_rng(seed)
@@ -73,16 +188,16 @@ def make_dataset(ctx, n, seed, forged_frac):
     sk[:, 0] &= 0x3F          # < 2^254 < r
     sk[:, 31] |= 1            # nonzero
     msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
-    sks = [bytes(r) for r in sk]
-    pks = ctx.public_keys(sks)
+    P = ctx.public_keys_raw(sk.tobytes())
     sign_msgs = msgs.copy()
     forged = np.zeros(n, dtype=bool)
     if forged_frac > 0:
         idx = rng.choice(n, size=max(1, int(n * forged_frac)), replace=False)
         forged[idx] = True
         sign_msgs[idx, 0] ^= 0xFF      # valid signature over a different message
-    sigs = ctx.sign(sks, [bytes(r) for r in sign_msgs])
-    return b"".join(sigs), b"".join(pks), msgs.tobytes(), forged
+    offs = np.arange(n + 1, dtype=np.uint64) * 32
+    S = ctx.sign_raw(sk.tobytes(), sign_msgs.tobytes(), offs)
+    return S, P, msgs.tobytes(), forged
 
 
 def make_keyed_dataset(ctx, n, k, seed, forged_frac):
@@ -93,8 +208,8 @@ def make_keyed_dataset(ctx, n, k, seed, forged_frac):
     sk = rng.integers(0, 256, size=(k, 32), dtype=np.uint8)
     sk[:, 0] &= 0x3F
     sk[:, 31] |= 1
-    sks = [bytes(r) for r in sk]
-    pks = ctx.public_keys(sks)
+    kp = ctx.public_keys_raw(sk.tobytes())
+    pks = [kp[96 * j:96 * j + 96] for j in range(k)]
     who = (np.arange(n) % k).astype(np.uint32)
     msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     sign_msgs = msgs.copy()
@@ -103,8 +218,9 @@ def make_keyed_dataset(ctx, n, k, seed, forged_frac):
         idx = rng.choice(n, size=max(1, int(n * forged_frac)), replace=False)
         forged[idx] = True
         sign_msgs[idx, 0] ^= 0xFF
-    sigs = ctx.sign([sks[w] for w in who], [bytes(r) for r in sign_msgs])
-    return b"".join(sigs), pks, who, msgs.tobytes(), forged
+    offs = np.arange(n + 1, dtype=np.uint64) * 32
+    S = ctx.sign_raw(sk[who].tobytes(), sign_msgs.tobytes(), offs)
+    return S, pks, who, msgs.tobytes(), forged
 
 
 def inject_adversarial(S, P, M, n, seed, frac=0.01):
@@ -132,68 +248,6 @@ def inject_adversarial(S, P, M, n, seed, frac=0.01):
         M[32 * i:32 * i + 32] = bytes.fromhex(c["msg"])
         expect[i] = c["code"]
     return bytes(S), bytes(P), bytes(M), expect, len(cases)
-
-
-def run_rlc(args, rank, world, local, dev):
-    """RLC batch mode (BASELINE config[3] shape): each rank holds n records
-    signed by `keys` distinct TEE keys; one RLC check per rank, Gt partials
-    all-gathered over RCCL and multiplied, bisection on failure.  Timed through
-    the host-buffer API (includes key dedup and PCIe transfers)."""
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    from cess_amd import bls
-    from cess_amd.dist import verify_rlc_sharded
-    n = args.n
-    ctx = bls.Context(device=local, max_batch=min(n, 1 << 20))
-    rng = np.random.default_rng((0x0A0D17, rank))
-    ksk = rng.integers(0, 256, size=(args.keys, 32), dtype=np.uint8)
-    ksk[:, 0] &= 0x3F
-    ksk[:, 31] |= 1
-    kpk = ctx.public_keys([bytes(r) for r in ksk])
-    owner = rng.integers(0, args.keys, size=n)
-    msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
-    sign_msgs = msgs.copy()
-    forged = rng.choice(n, size=args.forged_count, replace=False) if args.forged_count else np.array([], dtype=int)
-    sign_msgs[forged, 0] ^= 0xFF
-    sks = [bytes(ksk[o]) for o in owner]
-    sigs = ctx.sign(sks, [bytes(r) for r in sign_msgs])
-    S, P, M = b"".join(sigs), b"".join(kpk[o] for o in owner), msgs.tobytes()
-    offs = list(range(0, 32 * n + 1, 32))
-    seed = bytes(32)
-    for _ in range(args.warmup):
-        verify_rlc_sharded(ctx, S, P, M, offs, seed, rank, world, device=dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        codes, words, st = verify_rlc_sharded(ctx, S, P, M, offs, seed, rank, world, device=dev)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    expect = np.zeros(n, dtype=np.uint8)
-    expect[forged] = 5
-    ok = bool((np.frombuffer(codes, dtype=np.uint8) == expect).all())
-    if world > 1:
-        t = torch.tensor([elapsed, 1.0 if ok else 0.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.MIN)
-        elapsed, ok = float(t[0]), bool(t[1] == 1.0)
-    if rank == 0:
-        total = n * world * args.steps
-        print(json.dumps({
-            "metric": "verified BLS12-381 sigs/sec (node), RLC batch mode", "value": total / elapsed,
-            "unit": "sigs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u32", "data": "synthetic: few random keys, 32-byte msgs",
-            "config": {"workload": f"BASELINE config[3] shape: {n} sigs per GPU, {args.keys} distinct keys, "
-                                   f"{args.forged_count} forged per GPU, RLC + Gt-partial all-gather + bisection",
-                       "timing": "host-buffer API incl. key dedup and PCIe", "parallelism": f"shard-by-index x{world}"},
-            "verdicts_ok": ok, "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
-        }), flush=True)
-    ctx.close()
 
 
 CPU_LIB = os.path.join(ROOT, "tests", "hostemu", "libcpu_verify.so")
@@ -227,106 +281,209 @@ def cpu_baseline(S, M, P, idx, threads):
             "codes_ok": sum(1 for c in codes if c == 0)}
 
 
+# ---------------------------------------------------------------------------
+# rank body
+# ---------------------------------------------------------------------------
+def run_dry(args, rank, world):
+    """CPU rehearsal of the N>1 path: rendezvous of a 128-byte id through the
+    launcher's job directory, then the shard ranges of the config[2] batch from
+    the library's own cess_bls_shard_range (pure function, no device)."""
+    from cess_amd import bls
+    n_per = args.n or NPER_MULTI
+    n_total = n_per * world
+    if rank == 0:
+        rdv_put("comm_id", hashlib.sha256(b"dry" + os.urandom(16)).digest() * 4)
+    cid = rdv_get("comm_id")
+    b, e, w = bls.shard_range(n_total, world, rank)
+    rdv_put(f"shard_{rank}", json.dumps({"rank": rank, "begin": b, "end": e, "wpr": w,
+                                         "id": hashlib.sha256(cid).hexdigest()}).encode())
+    if rank == 0:
+        shards = [json.loads(rdv_get(f"shard_{r}")) for r in range(world)]
+        covered = sorted((s["begin"], s["end"]) for s in shards)
+        ok = covered[0][0] == 0 and covered[-1][1] == n_total and all(
+            covered[i][1] == covered[i + 1][0] for i in range(world - 1))
+        same_id = len({s["id"] for s in shards}) == 1
+        print(json.dumps({"dry_run": True, "n_gpus": world, "n_total": n_total, "sigs_per_gpu": n_per,
+                          "shards": shards, "cover_ok": ok, "same_comm_id": same_id}), flush=True)
+        rdv_put("done", b"1")
+    else:
+        rdv_get("done")
+    if rank == 0:
+        time.sleep(0.2)
+        rdv_cleanup(rank, world)
+
+
+def run_rlc(args, ctx, rank, world):
+    """RLC batch mode (BASELINE config[3] shape): each rank holds n records
+    signed by `keys` distinct TEE keys; one combination per rank, the Gt
+    partials all-gathered over RCCL and multiplied on the device inside the
+    library (cess_bls_verify_batch_rlc_sharded), bisection iff a rank's own
+    check fails.  Timed through the host-buffer API (key dedup + PCIe)."""
+    import numpy as np
+    n = args.n or (4 << 20)
+    rng = np.random.default_rng((0x0A0D17, rank))
+    ksk = rng.integers(0, 256, size=(args.keys, 32), dtype=np.uint8)
+    ksk[:, 0] &= 0x3F
+    ksk[:, 31] |= 1
+    kp = ctx.public_keys_raw(ksk.tobytes())
+    owner = rng.integers(0, args.keys, size=n)
+    msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sign_msgs = msgs.copy()
+    forged = rng.choice(n, size=args.forged_count, replace=False) if args.forged_count else np.array([], dtype=int)
+    sign_msgs[forged, 0] ^= 0xFF
+    offs = np.arange(n + 1, dtype=np.uint64) * 32
+    S = ctx.sign_raw(ksk[owner].tobytes(), sign_msgs.tobytes(), offs)
+    kpa = np.frombuffer(kp, dtype=np.uint8).reshape(args.keys, 96)
+    P, M = kpa[owner].tobytes(), msgs.tobytes()
+    offl = offs
+
+    def step():
+        if world > 1:
+            return ctx.verify_rlc_sharded(S, P, M, offl)          # seed: library CSPRNG
+        return ctx.verify_rlc(S, P, M, offl)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        ctx.comm_barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        codes, words, st = step()
+    ctx.synchronize()
+    if world > 1:
+        ctx.comm_barrier()
+    elapsed = time.perf_counter() - t0
+    expect = np.zeros(n, dtype=np.uint8)
+    expect[forged] = 5
+    ok = bool((np.frombuffer(codes, dtype=np.uint8) == expect).all())
+    if world > 1:
+        elapsed = ctx.comm_max(elapsed)
+        ok = ctx.comm_max(0.0 if ok else 1.0) == 0.0
+    if rank == 0:
+        total = n * world * args.steps
+        print(json.dumps({
+            "metric": "verified BLS12-381 sigs/sec (node), RLC batch mode", "value": total / elapsed,
+            "unit": "sigs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic: few random keys, 32-byte msgs",
+            "config": {"workload": f"BASELINE config[3] shape: {n} sigs per GPU, {args.keys} distinct keys, "
+                                   f"{args.forged_count} forged per GPU, RLC + Gt-partial RCCL all-gather + bisection",
+                       "timing": "host-buffer API incl. key dedup and PCIe", "parallelism": f"shard-by-index x{world}"},
+            "verdicts_ok": ok, "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
+            "runtime": runtime_provenance(),
+        }), flush=True)
+
+
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    from cess_amd import bls
-    from cess_amd.dist import gather_bitmap
-
-    if args.mode == "rlc":
-        run_rlc(args, rank, world, local, dev)
-        if world > 1:
-            dist.destroy_process_group()
+    if args.dry_run:
+        run_dry(args, rank, world)
         return
-    n = args.n
-    ctx = bls.Context(device=local, max_batch=n, profile=True)
+
+    # the library (and with it /opt/rocm's HIP runtime and RCCL) first
+    from cess_amd import bls
+    bls.load_library()
     import numpy as np
+
+    n = args.n or (N1_DEFAULT if world == 1 else NPER_MULTI)
+    if args.mode == "rlc":
+        ctx = bls.Context(device=local, max_batch=min(args.n or (4 << 20), 1 << 20))
+        if world > 1:
+            comm_setup(ctx, rank, world)
+        run_rlc(args, ctx, rank, world)
+        ctx.close()
+        return
+
+    ctx = bls.Context(device=local, max_batch=min(n, 1 << 20), profile=True)
+    if world > 1:
+        comm_setup(ctx, rank, world)
+    n_total = n * world
     keyed = args.mode == "keyed"
     if keyed:
         S, key_list, who, M, forged = make_keyed_dataset(ctx, n, args.keys, seed=(0x00C0FFEE, rank),
                                                          forged_frac=args.forged_frac)
         P = b"".join(key_list[w] for w in who)     # expanded records, for the CPU baseline only
         assert ctx.load_keys(key_list) == bytes(len(key_list))
-        d_idx = torch.from_numpy(who.astype(np.int32)).to(dev)
+        d_idx = ctx.to_device(who.astype(np.uint32))
     else:
         S, P, M, forged = make_dataset(ctx, n, seed=(0x00C0FFEE, rank), forged_frac=args.forged_frac)
     expect = np.where(forged, 5, 0).astype(np.uint8)
     n_adv_kinds = 0
     if args.mode == "adversarial":
         S, P, M, expect, n_adv_kinds = inject_adversarial(S, P, M, n, seed=(0xADD, rank))
-    d_sig = torch.frombuffer(bytearray(S), dtype=torch.uint8).to(dev)
-    d_pk = None if keyed else torch.frombuffer(bytearray(P), dtype=torch.uint8).to(dev)
-    d_msg = torch.frombuffer(bytearray(M), dtype=torch.uint8).to(dev)
-    d_off = (torch.arange(n + 1, dtype=torch.int64) * 32).to(dev)
-    d_codes = torch.empty(n, dtype=torch.uint8, device=dev)
-    d_bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    if world > 1:
+        b, e, wpr = bls.shard_range(n_total, world, rank)
+        assert (b, e) == (rank * n, rank * n + n), (b, e)
+    else:
+        wpr = (n + 63) // 64
+    d_sig = ctx.to_device(S)
+    d_pk = None if keyed else ctx.to_device(P)
+    d_msg = ctx.to_device(M)
+    d_off = ctx.to_device(np.arange(n + 1, dtype=np.uint64) * 32)
+    d_codes = ctx.device_alloc(world * wpr * 64)
+    d_bitmap = ctx.device_alloc(world * wpr * 8)
 
     def step():
         if keyed:
-            ctx.verify_keyed_device(n, d_sig.data_ptr(), d_idx.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
-                                    d_codes.data_ptr(), d_bitmap.data_ptr(), stream.cuda_stream)
+            ctx.verify_keyed_device(n, d_sig, d_idx, d_msg, d_off, d_codes, d_bitmap)
+        elif world > 1:
+            ctx.verify_sharded_device(n_total, d_sig, d_pk, d_msg, d_off, d_codes, d_bitmap)
         else:
-            ctx.verify_device(n, d_sig.data_ptr(), d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
-                              d_codes.data_ptr(), d_bitmap.data_ptr(), stream.cuda_stream)
-        return gather_bitmap(d_bitmap, n * world, world) if world > 1 else d_bitmap
+            ctx.verify_device(n, d_sig, d_pk, d_msg, d_off, d_codes, d_bitmap)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    ctx.synchronize()
     ctx.stage_times(reset=True)
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+        ctx.comm_barrier()
+    ctx.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        full = step()
-    torch.cuda.synchronize()
+        step()
+    ctx.synchronize()
     if world > 1:
-        dist.barrier()
+        ctx.comm_barrier()
     elapsed = time.perf_counter() - t0
     stages = ctx.stage_times(reset=True)   # HIP events on the launch stream, timed region only
     if keyed:   # the keyed pipeline runs k_merge_pk in k_decode_pk's slot and has no per-signature prepare
         stages["k_merge_pk"] = stages.pop("k_decode_pk")
         stages.pop("k_prepare", None)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = ctx.comm_max(elapsed)
 
-    # correctness of the last step: local codes + the gathered bitmap
-    codes = d_codes.cpu().numpy()
-    local_ok = bool((codes == expect).all())     # bit-exact per-record codes
-    popcount = int(sum(bin(int(w) & ((1 << 64) - 1)).count("1") for w in full.cpu().tolist()))
-    ok_t = torch.tensor([1 if local_ok else 0], device=dev)
-    if world > 1:
-        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+    # correctness of the last step: this rank's codes + the gathered bitmap
+    codes_all = np.frombuffer(ctx.from_device(d_codes, world * wpr * 64), dtype=np.uint8)
+    my = codes_all[rank * wpr * 64: rank * wpr * 64 + n] if world > 1 else codes_all[:n]
+    local_ok = bool((my == expect).all())                 # bit-exact per-record codes
+    words = np.frombuffer(ctx.from_device(d_bitmap, world * wpr * 8), dtype=np.uint64)
+    popcount = int(np.unpackbits(words.view(np.uint8)).sum())
+    ok = local_ok if world == 1 else ctx.comm_max(0.0 if local_ok else 1.0) == 0.0
 
     if rank == 0:
-        total = n * world * args.steps
+        total = n_total * args.steps
         value = total / elapsed
         oc = load_opcount()
         per = oc["per_stage"]
         whole_mads = oc["algorithmic_mads_per_sig"]
         if keyed:   # per-key decode + prepare are done once per key, outside the per-signature work
             whole_mads -= sum((per[k]["mul"] + per[k]["sqr"]) * ALG_MADS_PER_FP_MUL for k in ("k_decode_pk", "k_prepare"))
+        chunk = min(n, ctx.max_batch)
+        launches = args.steps * ((n + chunk - 1) // chunk)
         dom = max(stages, key=lambda k: stages[k])
-        dom_ms = stages[dom] / args.steps                  # per launch (one launch per step, chunk = n)
-        alg = (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL * n
+        dom_ms = stages[dom] / launches                   # per launch (chunk records each)
+        alg = (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL * chunk
         achieved = alg / (dom_ms * 1e-3)
-        pmc = load_pmc_traffic()
+        sha = lib_sha256()
+        pmc = load_pmc_traffic(sha)
         traffic = None
-        if pmc and pmc.get("n") == n:
+        if pmc and pmc.get("n") == chunk:
             traffic = (pmc.get("all", {}).get(dom) or {}).get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and args.cpu_sample > 0:
@@ -334,6 +491,16 @@ def main():
             rr = random.Random(5)
             idx = rr.sample(range(n), min(n, args.cpu_sample))
             cpu = cpu_baseline(S, M, P, idx, args.cpu_threads)
+        if args.mode == "persig":
+            wl = (f"BASELINE config[1]: {n} independent sigs, distinct keys, per-sig 2-pairing verify" if world == 1
+                  else f"BASELINE config[2] shape: {n_total} sigs ({n} per GPU) sharded by index across {world} GPUs, "
+                       f"distinct keys, per-sig 2-pairing verify, RCCL all-gather of verdict bitmap + codes")
+        elif keyed:
+            wl = (f"BASELINE config[3] shape, per-signature verdicts: {n} sigs per GPU over {args.keys} keys, key "
+                  f"decode + G2Prepared once per key (keyed batch)")
+        else:
+            wl = (f"BASELINE config[4] shape: {n} sigs per GPU, 1% invalid (half forged, half {n_adv_kinds} kinds of "
+                  f"malformed/non-subgroup/identity records), exact codes")
         rec = {
             "metric": "verified BLS12-381 sigs/sec (node)",
             "value": value,
@@ -347,30 +514,26 @@ def main():
             "vs_baseline": None,
             "dtype": "u32 (381-bit Montgomery, 14x28-bit limb products via v_mad_u64_u32)",
             "data": "synthetic: random distinct keys + 32-byte messages, keys/sigs generated on GPU",
-            "config": {"workload": (f"BASELINE config[1]: {n} independent sigs per GPU, distinct keys, "
-                                    f"per-sig 2-pairing verify" if args.mode == "persig" else
-                                    f"BASELINE config[3] shape, per-signature verdicts: {n} sigs per GPU over "
-                                    f"{args.keys} keys, key decode + G2Prepared once per key (keyed batch)"
-                                    if keyed else
-                                    f"BASELINE config[4] shape: {n} sigs per GPU, 1% invalid (half forged, half "
-                                    f"{n_adv_kinds} kinds of malformed/non-subgroup/identity records), exact codes")
-                                   + (", RCCL allgather of verdict bitmap" if world > 1 else ""),
-                       "sigs_per_gpu": n, "msg_bytes": 32, "forged_frac": args.forged_frac,
-                       "parallelism": f"shard-by-index x{world}"},
-            "verdicts_ok": bool(ok_t.item() == 1),
+            "config": {"workload": wl, "sigs_per_gpu": n, "sigs_total": n_total, "msg_bytes": 32,
+                       "forged_frac": args.forged_frac, "parallelism": f"shard-by-index x{world}",
+                       "launch_chunk": chunk},
+            "verdicts_ok": ok,
             "bitmap_popcount": popcount,
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": achieved / 1e12, "peak": PEAK_MADS / 1e12,
                          "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
                          "frac": achieved / PEAK_MADS, "traffic": traffic,
+                         "traffic_source": pmc["_file"] if pmc else None,
                          "alg_mads_per_sig": (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL,
                          "whole_path_frac": whole_mads * value / world / PEAK_MADS},
             "cpu_baseline": cpu,
+            "runtime": dict(runtime_provenance(), lib_sha256=sha),
         }
         print(json.dumps(rec), flush=True)
+    for d in (d_sig, d_pk, d_msg, d_off, d_codes, d_bitmap) + ((d_idx,) if keyed else ()):
+        if d:
+            ctx.device_free(d)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

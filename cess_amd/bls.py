@@ -40,7 +40,16 @@ EXPORTS = (
     "cess_bls_status_string", "cess_bls_version",
     "cess_bls_verify_batch_rlc", "cess_bls_rlc_begin", "cess_bls_gt_product_is_one", "cess_bls_rlc_finish",
     "cess_bls_keys_load", "cess_bls_verify_batch_keyed", "cess_bls_verify_batch_keyed_device",
+    "cess_bls_comm_id", "cess_bls_comm_init", "cess_bls_shard_range", "cess_bls_verify_batch_sharded",
+    "cess_bls_verify_batch_sharded_device", "cess_bls_verify_batch_rlc_sharded", "cess_bls_comm_barrier",
+    "cess_bls_comm_max_f64", "cess_bls_device_alloc", "cess_bls_device_free", "cess_bls_copy_to_device",
+    "cess_bls_copy_from_device", "cess_bls_synchronize", "cess_bls_enclave_verify_bls",
 )
+
+# infrastructure status codes (include/cess_bls.h)
+E_INVALID_ARG, E_NO_DEVICE, E_HIP, E_OOM, E_RCCL, E_BUSY, E_BAD_KEY, E_BAD_SIG, E_NO_COMM = range(-1, -10, -1)
+F_PROFILE, F_STRICT_IDENTITY = 1, 2
+MODE_PER_SIG, MODE_RLC = 0, 1
 
 
 class DeviceUnavailable(RuntimeError):
@@ -48,11 +57,14 @@ class DeviceUnavailable(RuntimeError):
 
 
 class BlsInfraError(RuntimeError):
-    pass
+    def __init__(self, msg, status=None):
+        super().__init__(msg)
+        self.status = status
 
 
 class _Config(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("max_batch", ctypes.c_uint64), ("flags", ctypes.c_uint32)]
+    _fields_ = [("device", ctypes.c_int), ("max_batch", ctypes.c_uint64), ("flags", ctypes.c_uint32),
+                ("mode", ctypes.c_uint32), ("n_devices", ctypes.c_int), ("devices", ctypes.POINTER(ctypes.c_int))]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -91,6 +103,21 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_gt_product_is_one.argtypes = [vp, sz, _u8p, ctypes.POINTER(ctypes.c_int)]
         lib.cess_bls_rlc_finish.argtypes = [vp, ctypes.c_int, _u8p, _u64p, _u64p]
         lib.cess_bls_verify_batch_rlc.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p, _u64p, _u64p]
+        lib.cess_bls_comm_id.argtypes = [_u8p]
+        lib.cess_bls_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, _u8p]
+        lib.cess_bls_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _u64p, _u64p, _u64p]
+        lib.cess_bls_verify_batch_sharded.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u64p]
+        lib.cess_bls_verify_batch_sharded_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
+        lib.cess_bls_verify_batch_rlc_sharded.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p, _u64p, _u64p,
+                                                          ctypes.POINTER(ctypes.c_int)]
+        lib.cess_bls_comm_barrier.argtypes = [vp]
+        lib.cess_bls_comm_max_f64.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        lib.cess_bls_device_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
+        lib.cess_bls_device_free.argtypes = [vp, vp]
+        lib.cess_bls_copy_to_device.argtypes = [vp, vp, vp, sz]
+        lib.cess_bls_copy_from_device.argtypes = [vp, vp, vp, sz]
+        lib.cess_bls_synchronize.argtypes = [vp]
+        lib.cess_bls_enclave_verify_bls.argtypes = [vp, _u8p, sz, _u8p, sz, _u8p, sz, ctypes.POINTER(ctypes.c_int)]
         lib.cess_bls_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                              ctypes.c_int, ctypes.c_int]
         lib.cess_bls_status_string.restype = ctypes.c_char_p
@@ -106,6 +133,17 @@ def _buf(b: bytes):
     return ctypes.cast(ctypes.c_char_p(bytes(b)), _u8p)
 
 
+def _u64arr(x):
+    """uint64 array argument: numpy arrays are passed without a copy (the
+    caller keeps them alive for the call), sequences are converted."""
+    if hasattr(x, "ctypes") and getattr(x, "dtype", None) is not None:
+        import numpy as np
+        a = np.ascontiguousarray(x, dtype=np.uint64)
+        return (ctypes.c_uint64 * len(a)).from_buffer(a) if a.flags.writeable else \
+            (ctypes.c_uint64 * len(a)).from_buffer_copy(a)
+    return (ctypes.c_uint64 * len(x))(*x)
+
+
 def _offsets(lengths: Sequence[int]):
     arr = (ctypes.c_uint64 * (len(lengths) + 1))()
     acc = 0
@@ -119,10 +157,17 @@ def _offsets(lengths: Sequence[int]):
 class Context:
     """One GPU: device buffers, stream and the -G2 prepared table."""
 
-    def __init__(self, device: int = 0, max_batch: int = 1 << 20, profile: bool = False):
+    def __init__(self, device: int = 0, max_batch: int = 1 << 20, profile: bool = False,
+                 strict_identity: bool = False, mode: int = MODE_PER_SIG, devices: Optional[Sequence[int]] = None):
+        """devices: a list of >1 ordinals makes one context over several GPUs of
+        this process (host-buffer batches sharded by index across them)."""
         lib = load_library()
         self._lib = lib
-        cfg = _Config(device, max_batch, 1 if profile else 0)
+        flags = (F_PROFILE if profile else 0) | (F_STRICT_IDENTITY if strict_identity else 0)
+        ndev = len(devices) if devices is not None and len(devices) > 1 else 0
+        self._devs = (ctypes.c_int * max(ndev, 1))(*(devices if ndev else [0]))
+        cfg = _Config(device, max_batch, flags, mode, ndev, self._devs if ndev else None)
+        self._keys_owner = None      # None | "user" | "verify_batch": who loaded the key table
         h = ctypes.c_void_p()
         st = lib.cess_bls_ctx_create(ctypes.byref(cfg), ctypes.byref(h))
         if st != 0:
@@ -147,7 +192,7 @@ class Context:
 
     def _chk(self, st):
         if st != 0:
-            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode())
+            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode(), st)
 
     @property
     def handle(self):
@@ -179,7 +224,7 @@ class Context:
         """Fixed-stride batch over packed host buffers; returns (codes, bitmap words)."""
         n = len(sigs) // 48
         assert len(sigs) == 48 * n and len(pks) == 96 * n
-        offs = (ctypes.c_uint64 * (n + 1))(*msg_offsets)
+        offs = _u64arr(msg_offsets)
         codes = (ctypes.c_uint8 * max(n, 1))()
         bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
         self._chk(self._lib.cess_bls_verify_batch(self._h, n, _buf(sigs), _buf(pks), _buf(msgs), offs, codes, bitmap))
@@ -201,10 +246,11 @@ class Context:
                                                          d_bitmap, stream or None))
 
     # --- distinct-key table (per-key decode + G2Prepared done once) -------
-    def load_keys(self, keys: Sequence[bytes]) -> bytes:
+    def load_keys(self, keys: Sequence[bytes], _owner: str = "user") -> bytes:
         """Decode and prepare each distinct 96-byte key once (PublicKey::deserialize,
         src/lib.rs:68-82, and G2Prepared::from, :88); returns the per-key codes
         (0, or 4 = PK_POINT).  Replaces any previously loaded table."""
+        self._keys_owner = _owner
         k = len(keys)
         assert all(len(bytes(x)) == 96 for x in keys)
         kc = (ctypes.c_uint8 * max(k, 1))()
@@ -216,8 +262,20 @@ class Context:
         key_idx[i]; same codes as the per-record path on the expanded records."""
         n = len(sigs) // 48
         assert len(sigs) == 48 * n and len(key_idx) == n
+        if self._keys_owner != "user":
+            raise BlsInfraError("no user-loaded key table on this context (load_keys first; verify_batch's "
+                                "internal table is never used for caller indices)", E_INVALID_ARG)
         idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
-        offs = (ctypes.c_uint64 * (n + 1))(*msg_offsets)
+        offs = _u64arr(msg_offsets)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        self._chk(self._lib.cess_bls_verify_batch_keyed(self._h, n, _buf(sigs), idx, _buf(msgs), offs, codes, bitmap))
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64]
+
+    def _verify_keyed_any(self, sigs, key_idx, msgs, msg_offsets):
+        n = len(sigs) // 48
+        idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        offs = _u64arr(msg_offsets)
         codes = (ctypes.c_uint8 * max(n, 1))()
         bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
         self._chk(self._lib.cess_bls_verify_batch_keyed(self._h, n, _buf(sigs), idx, _buf(msgs), offs, codes, bitmap))
@@ -225,17 +283,20 @@ class Context:
 
     def verify_keyed_device(self, n, d_sigs, d_key_idx, d_msgs, d_offs, d_codes, d_bitmap, stream=0):
         """Device-resident keyed batch (HBM pointers as ints); not synchronised."""
+        if self._keys_owner != "user":
+            raise BlsInfraError("no user-loaded key table on this context", E_INVALID_ARG)
         self._chk(self._lib.cess_bls_verify_batch_keyed_device(self._h, n, d_sigs, d_key_idx, d_msgs, d_offs,
                                                                d_codes, d_bitmap, stream or None))
 
     # --- RLC batch mode (random linear combination + bisection) ----------
-    def rlc_begin(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: bytes) -> bytes:
+    def rlc_begin(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: Optional[bytes] = None) -> bytes:
         """Decode, hash and scale a fixed-stride batch, run its RLC check and
         return this shard's Gt partial (576 canonical bytes).  The buffers are
         kept alive until rlc_finish."""
         n = len(sigs) // 48
-        assert len(sigs) == 48 * n and len(pks) == 96 * n and len(seed) == 32
-        keep = (_buf(sigs), _buf(pks), _buf(msgs), (ctypes.c_uint64 * (n + 1))(*msg_offsets), _buf(seed))
+        assert len(sigs) == 48 * n and len(pks) == 96 * n and (seed is None or len(seed) == 32)
+        keep = (_buf(sigs), _buf(pks), _buf(msgs), _u64arr(msg_offsets),
+                _buf(seed) if seed is not None else None)
         self._rlc_keep = keep
         self._rlc_n = n
         gt = (ctypes.c_uint8 * 576)()
@@ -265,17 +326,116 @@ class Context:
         """Single-GPU RLC batch verification -> (codes, bitmap, stats); codes equal
         verify_fixed's (soundness error 2^-127 per check)."""
         n = len(sigs) // 48
-        seed = seed if seed is not None else secrets.token_bytes(32)
-        offs = (ctypes.c_uint64 * (n + 1))(*msg_offsets)
+        offs = _u64arr(msg_offsets)
         codes = (ctypes.c_uint8 * max(n, 1))()
         bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
         st = (ctypes.c_uint64 * 4)()
+        # seed None: the library draws it from the OS CSPRNG (it must be secret
+        # and unpredictable to the signers, include/cess_bls.h)
+        sd = _buf(seed) if seed is not None else None
         self._chk(self._lib.cess_bls_verify_batch_rlc(self._h, n, _buf(sigs), _buf(pks), _buf(msgs), offs,
-                                                      _buf(seed), codes, bitmap, st))
+                                                      sd, codes, bitmap, st))
         stats = {"checks": st[0], "leaves": st[1], "leaf_sigs": st[2], "distinct_keys": st[3]}
         return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64], stats
 
+    # --- RCCL communicator (one process per GPU) ------------------------
+    def comm_init(self, nranks: int, rank: int, comm_id: bytes):
+        """ncclCommInitRank on this context's device (collective)."""
+        assert len(comm_id) == 128
+        self._chk(self._lib.cess_bls_comm_init(self._h, nranks, rank, _buf(comm_id)))
+        self.nranks, self.rank = nranks, rank
+
+    def verify_sharded(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets) -> Tuple[bytes, list]:
+        """Every rank passes the whole fixed-stride batch; returns the verdicts
+        of all records (each rank verifies its shard, RCCL all-gathers)."""
+        n = len(sigs) // 48
+        offs = _u64arr(msg_offsets)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        self._chk(self._lib.cess_bls_verify_batch_sharded(self._h, n, _buf(sigs), _buf(pks), _buf(msgs), offs, codes,
+                                                          bitmap))
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64]
+
+    def verify_sharded_device(self, n_total, d_sigs, d_pks, d_msgs, d_offs, d_codes_all, d_bitmap_all, stream=0):
+        """Device-resident sharded batch (this rank's shard in HBM); not synchronised."""
+        self._chk(self._lib.cess_bls_verify_batch_sharded_device(self._h, n_total, d_sigs, d_pks, d_msgs, d_offs,
+                                                                 d_codes_all or None, d_bitmap_all, stream or None))
+
+    def verify_rlc_sharded(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, seed: Optional[bytes] = None):
+        """RLC over the communicator for this rank's shard -> (codes, bitmap, stats)."""
+        n = len(sigs) // 48
+        offs = _u64arr(msg_offsets)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        st = (ctypes.c_uint64 * 4)()
+        g = ctypes.c_int()
+        self._chk(self._lib.cess_bls_verify_batch_rlc_sharded(self._h, n, _buf(sigs), _buf(pks), _buf(msgs), offs,
+                                                              _buf(seed) if seed is not None else None, codes, bitmap,
+                                                              st, ctypes.byref(g)))
+        stats = {"checks": st[0], "leaves": st[1], "leaf_sigs": st[2], "distinct_keys": st[3], "global_ok": bool(g.value)}
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64], stats
+
+    def comm_barrier(self):
+        self._chk(self._lib.cess_bls_comm_barrier(self._h))
+
+    def comm_max(self, v: float) -> float:
+        d = ctypes.c_double(v)
+        self._chk(self._lib.cess_bls_comm_max_f64(self._h, ctypes.byref(d)))
+        return d.value
+
+    # --- device memory on this context's GPU -------------------------------
+    def device_alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        self._chk(self._lib.cess_bls_device_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def device_free(self, d: int):
+        self._chk(self._lib.cess_bls_device_free(self._h, d))
+
+    def to_device(self, data, d: Optional[int] = None) -> int:
+        """Copy a bytes-like / numpy buffer to HBM (allocating when d is None)."""
+        mv = memoryview(data).cast("B")
+        if d is None:
+            d = self.device_alloc(len(mv))
+        if len(mv):
+            src = (ctypes.c_uint8 * len(mv)).from_buffer_copy(mv) if mv.readonly else (ctypes.c_uint8 * len(mv)).from_buffer(mv)
+            self._chk(self._lib.cess_bls_copy_to_device(self._h, d, src, len(mv)))
+        return d
+
+    def from_device(self, d: int, nbytes: int) -> bytes:
+        out = (ctypes.c_uint8 * max(nbytes, 1))()
+        self._chk(self._lib.cess_bls_copy_from_device(self._h, out, d, nbytes))
+        return bytes(out)[:nbytes]
+
+    def synchronize(self):
+        self._chk(self._lib.cess_bls_synchronize(self._h))
+
+    # --- cp_enclave_verify::verify_bls (primitives/enclave-verify/src/lib.rs:230-235)
+    def enclave_verify_bls(self, key: bytes, msg: bytes, sig: bytes) -> bool:
+        """Reversed argument order as the reference; raises BlsInfraError with
+        status E_BAD_KEY / E_BAD_SIG where the reference panics (key first)."""
+        ok = ctypes.c_int()
+        key, msg, sig = bytes(key), bytes(msg), bytes(sig)
+        self._chk(self._lib.cess_bls_enclave_verify_bls(self._h, _buf(key), len(key), _buf(msg), len(msg), _buf(sig),
+                                                        len(sig), ctypes.byref(ok)))
+        return bool(ok.value)
+
     # --- generator side -------------------------------------------------
+    def public_keys_raw(self, sks: bytes) -> bytes:
+        """n concatenated 32-byte secret keys -> n concatenated 96-byte keys."""
+        n = len(sks) // 32
+        out = (ctypes.c_uint8 * (96 * max(n, 1)))()
+        self._chk(self._lib.cess_bls_public_key_batch(self._h, n, _buf(sks), out))
+        return bytes(out)[: 96 * n]
+
+    def sign_raw(self, sks: bytes, msgs: bytes, msg_offsets) -> bytes:
+        """Fixed arrays in, 48-byte signatures out (concatenated)."""
+        n = len(sks) // 32
+        offs = _u64arr(msg_offsets)
+        out = (ctypes.c_uint8 * (48 * max(n, 1)))()
+        self._chk(self._lib.cess_bls_sign_batch(self._h, n, _buf(sks), _buf(msgs), offs, out))
+        return bytes(out)[: 48 * n]
+
     def public_keys(self, sks: Sequence[bytes]) -> list:
         n = len(sks)
         out = (ctypes.c_uint8 * (96 * max(n, 1)))()
@@ -307,6 +467,26 @@ class Context:
 
 
 _default: Optional[Context] = None
+
+
+def shard_range(n: int, nranks: int, rank: int) -> Tuple[int, int, int]:
+    """(begin, end, words_per_rank) of rank's shard (cess_bls_shard_range)."""
+    lib = load_library()
+    b, e, w = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    st = lib.cess_bls_shard_range(n, nranks, rank, ctypes.byref(b), ctypes.byref(e), ctypes.byref(w))
+    if st != 0:
+        raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
+    return b.value, e.value, w.value
+
+
+def comm_id() -> bytes:
+    """ncclGetUniqueId (128 bytes) for cess_bls_comm_init; call on one rank."""
+    lib = load_library()
+    out = (ctypes.c_uint8 * 128)()
+    st = lib.cess_bls_comm_id(out)
+    if st != 0:
+        raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
+    return bytes(out)
 
 
 def default_context() -> Context:
@@ -482,25 +662,26 @@ def verify_batch(records: Iterable[Tuple[bytes, bytes, bytes]], ctx: Optional[Co
     With dedup_keys, a fixed-size batch whose records share few keys (at most
     one distinct key per 8 records, e.g. TEE-signed audit verdicts) runs the
     keyed path: each distinct key is decoded and prepared once
-    (cess_bls_keys_load, replacing the context's key table).  Codes are the
-    same as the per-record path (tests/test_gpu_keyed.py)."""
+    (cess_bls_keys_load).  A context whose key table a caller loaded
+    (Context.load_keys) is never overwritten: then the batch runs the
+    per-record path.  Codes are the same either way (tests/test_gpu_keyed.py)."""
     records = list(records)
     ctx = ctx or default_context()
     n = len(records)
     codes = None
-    if dedup_keys and n >= 256 and all(len(r[0]) == 48 and len(r[2]) == 96 for r in records):
+    if dedup_keys and ctx._keys_owner != "user" and n >= 256 and all(len(r[0]) == 48 and len(r[2]) == 96 for r in records):
         kid = {}
         for r in records:
             kid.setdefault(bytes(r[2]), len(kid))
             if 8 * len(kid) > n:
                 break
         if 8 * len(kid) <= n:
-            ctx.load_keys(list(kid))
+            ctx.load_keys(list(kid), _owner="verify_batch")
             msgs = [bytes(r[1]) for r in records]
             offs = [0]
             for m in msgs:
                 offs.append(offs[-1] + len(m))
-            codes, _ = ctx.verify_keyed(b"".join(bytes(r[0]) for r in records), [kid[bytes(r[2])] for r in records],
+            codes, _ = ctx._verify_keyed_any(b"".join(bytes(r[0]) for r in records), [kid[bytes(r[2])] for r in records],
                                         b"".join(msgs), offs)
     if codes is None:
         codes = ctx.verify_codes(records)

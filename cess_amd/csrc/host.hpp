@@ -1,0 +1,170 @@
+// Internal declarations shared by the host translation units behind
+// include/cess_bls.h (host.cpp: per-device context and the per-signature
+// pipeline; host_rlc.cpp: RLC batch mode; host_multi.cpp: RCCL communicator,
+// sharded batches and multi-device contexts).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/cess_bls.h"
+#include "kernels.hpp"
+
+// kernels (k_*.hip)
+__global__ void k_decode_sig(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*, uint32_t*, uint64_t);
+__global__ void k_decode_pk(uint64_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*, uint32_t*, uint64_t, uint32_t);
+__global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*, uint32_t*, uint64_t);
+__global__ void k_prepare(uint64_t, const uint32_t*, uint4*, uint64_t);
+__global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                         const uint4*, uint4*, uint4*, uint64_t, const uint32_t*, uint64_t);
+__global__ void k_merge_pk(uint64_t, const uint32_t*, uint32_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*);
+__global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
+__global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
+__global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
+__global__ void k_hash_out(uint64_t, const uint8_t*, const uint64_t*, uint8_t*);
+// RLC batch mode (k_rlc.hip)
+__global__ void k_rlc_scale(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                            uint64_t, uint32_t*, uint32_t*, uint64_t, uint64_t);
+__global__ void k_gt_prod(uint32_t, const uint8_t*, uint4*, uint8_t*);
+__global__ void k_g1_sum_segs(uint32_t, const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*, uint64_t,
+                              uint32_t*, uint64_t);
+__global__ void k_rlc_pairs_list(uint32_t, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint8_t*, uint8_t*,
+                                 uint8_t*, uint32_t*, uint32_t*, const uint32_t*);
+__global__ void k_fp12_prod_segs(uint32_t, const uint32_t*, const uint4*, uint64_t, uint4*, uint4*);
+
+namespace cess_host {
+
+enum Stage { ST_DECODE_SIG, ST_DECODE_PK, ST_HASH, ST_PREPARE, ST_MILLER, ST_FINAL, ST_N };
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want) {
+    if (want <= bytes) return CESS_BLS_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, want) != hipSuccess) return CESS_BLS_E_OOM;
+    bytes = want;
+    return CESS_BLS_OK;
+  }
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// State of one RLC batch between cess_bls_rlc_begin and cess_bls_rlc_finish.
+struct RlcState {
+  uint64_t n = 0;
+  const uint8_t *sigs = nullptr, *pks = nullptr, *msgs = nullptr;   // caller's records (kept valid by the caller)
+  const uint64_t* offs = nullptr;
+  std::vector<uint8_t> codes;       // decode codes; 0 = candidate for the pairing check
+  std::vector<uint32_t> perm;       // record indices sorted by key group
+  std::vector<uint64_t> gbeg;       // K + 1 group boundaries in perm
+  uint32_t K = 0;
+  bool local_ok = false;
+  bool per_sig = false;             // too many distinct keys for a combination: verified per signature
+  uint64_t checks = 0, leaves = 0, leaf_sigs = 0;
+  DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
+  DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, rec_f2, acc, slots, fin_code, fin_bm, gt, gts, tmp;
+  DevBuf seg, part2, rec_coeffs, lists, d_gt_all;
+};
+
+}  // namespace cess_host
+
+struct cess_bls_ctx {
+  int device = 0;
+  uint64_t cap = 0;
+  uint32_t flags = 0;
+  uint32_t mode = CESS_BLS_MODE_PER_SIG;
+  hipStream_t stream = nullptr;
+  // stage buffers (SoA, stride = cap)
+  cess_host::DevBuf pre, code, inf, sig_aff, pk_aff, h_aff, coeffs, fval, fe_slots, bitmap, neg_g2;
+  // staging for the host-buffer APIs
+  cess_host::DevBuf in_sigs, in_pks, in_msgs, in_offs, out_gt, in_sks, out_bytes;
+  // profiling
+  hipEvent_t ev[cess_host::ST_N + 1] = {};
+  double stage_ms[cess_host::ST_N] = {};
+  cess_host::RlcState* rlc = nullptr;
+  // distinct-key table (cess_bls_keys_load): decoded keys + G2Prepared rows, stride = nkeys
+  uint32_t nkeys = 0;
+  cess_host::DevBuf key_in, key_code, key_inf, key_aff, key_coeffs, in_idx;
+  // ordering of successive calls on possibly different streams: every entry
+  // point waits for the previous call's work (done_ev on last_stream)
+  hipEvent_t done_ev = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool pending = false;
+  // one host thread at a time (the ABI contract); a second concurrent caller
+  // gets CESS_BLS_E_BUSY instead of racing on the context buffers
+  std::mutex busy;
+  // RCCL communicator (cess_bls_comm_init): one rank per process and GPU
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  cess_host::DevBuf comm_buf, comm_words, comm_codes;
+  // multi-device context (cess_bls_config.n_devices > 1): one sub-context per
+  // device, batches sharded by index across them from host threads
+  std::vector<cess_bls_ctx*> subs;
+};
+
+#define HIPCHK(x)                                 \
+  do {                                            \
+    if ((x) != hipSuccess) return CESS_BLS_E_HIP; \
+  } while (0)
+
+namespace cess_host {
+
+// RAII guard for the one-thread-at-a-time contract
+struct CtxLock {
+  std::unique_lock<std::mutex> lk;
+  explicit CtxLock(cess_bls_ctx* c) : lk(c->busy, std::try_to_lock) {}
+  bool ok() const { return lk.owns_lock(); }
+};
+
+// make stream s wait for the previous call's work; called by every entry point
+// before it enqueues anything (the context buffers are shared across calls)
+int order_begin(cess_bls_ctx* c, hipStream_t s);
+// record the end of this call's work on s
+int order_end(cess_bls_ctx* c, hipStream_t s);
+
+int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+              const uint64_t* offs, const uint8_t* pre, uint8_t* codes, uint64_t* bitmap, uint8_t* gt);
+int verify_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                const uint64_t* offs, const uint8_t* pre, uint8_t* codes_out, uint64_t* bitmap_out, uint8_t* gt_out);
+int verify_var_host(cess_bls_ctx* c, size_t n, const uint8_t* sig_data, const uint64_t* sig_offsets,
+                    const uint8_t* pk_data, const uint64_t* pk_offsets, const uint8_t* msgs, const uint64_t* msg_offsets,
+                    uint8_t* codes_out, uint64_t* bitmap_out);
+int collect_profile(cess_bls_ctx* c, hipStream_t s);
+// RLC (host_rlc.cpp)
+int rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+              const uint64_t* offs, const uint8_t* seed32, uint8_t* gt_out);
+// index_hi: added to every record index of the scalar derivation (shard k
+// passes k << 40, so shards never share an r_i under one seed)
+int rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                 const uint64_t* offs, const uint8_t* seed32, uint64_t index_hi, uint8_t* gt_out);
+int rlc_finish(cess_bls_ctx* c, uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4);
+int gt_product_is_one(cess_bls_ctx* c, size_t m, const uint8_t* gts, bool gts_on_device, int* is_one);
+int verify_rlc_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                    const uint64_t* offs, const uint8_t* seed32, uint8_t* codes_out, uint64_t* bitmap_out,
+                    uint64_t* stats4);
+// OS randomness for RLC seeds drawn by the library (mode = RLC)
+int os_random(uint8_t* out, size_t n);
+// shard of a batch for rank r of R (whole bitmap words, equal word count per rank)
+void shard_of(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end, uint64_t* words_per_rank);
+// bitmap words from codes (host)
+void bitmap_from_codes(const uint8_t* codes, uint64_t n, uint64_t* words);
+
+}  // namespace cess_host

@@ -1,0 +1,357 @@
+// Multi-GPU paths of include/cess_bls.h.
+//
+// Signatures are independent (reference src/lib.rs:243 is per signature), so a
+// batch shards by index with no exchange during compute.  Two deployments:
+//
+//  * one process per GPU (cess_bls_comm_init): the context owns an RCCL
+//    communicator; the sharded entry points verify the rank's shard and
+//    all-gather the verdict-bitmap words (and code bytes, and in RLC mode the
+//    576-byte Gt partials) over xGMI with ncclAllGather.  Shards are whole
+//    bitmap words with an equal word count per rank, so the all-gather is in
+//    place and needs no re-packing.
+//  * one process driving several GPUs (cess_bls_config.n_devices > 1): the
+//    context holds one sub-context per device and the host-buffer batches are
+//    split the same way across them, one host thread per device, each writing
+//    its verdicts straight into the caller's buffers (no collective needed in
+//    one address space).
+#include <thread>
+
+#include "host.hpp"
+
+using namespace cess_host;
+
+#define NCCLCHK(x)                                 \
+  do {                                             \
+    if ((x) != ncclSuccess) return CESS_BLS_E_RCCL; \
+  } while (0)
+
+#define ENTRY(c)                          \
+  if (!(c)) return CESS_BLS_E_INVALID_ARG; \
+  CtxLock lock_(c);                        \
+  if (!lock_.ok()) return CESS_BLS_E_BUSY
+
+// single-device workers (host.cpp)
+int cess_keys_load_one(cess_bls_ctx* c, size_t k, const uint8_t* pks, uint8_t* key_codes_out);
+int cess_keyed_one(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint32_t* key_idx, const uint8_t* msgs,
+                   const uint64_t* offs, uint8_t* codes_out, uint64_t* bitmap_out);
+int cess_gen_one(cess_bls_ctx* c, int kind, size_t n, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs,
+                 uint8_t* out);
+
+// ---------------------------------------------------------------------------
+// one process per GPU: RCCL communicator
+// ---------------------------------------------------------------------------
+extern "C" int cess_bls_shard_range(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end,
+                                    uint64_t* words_per_rank) {
+  if (nranks <= 0 || rank < 0 || rank >= nranks) return CESS_BLS_E_INVALID_ARG;
+  shard_of(n, nranks, rank, begin, end, words_per_rank);
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_comm_id(uint8_t id_out[CESS_BLS_COMM_ID_BYTES]) {
+  if (!id_out) return CESS_BLS_E_INVALID_ARG;
+  static_assert(sizeof(ncclUniqueId) == CESS_BLS_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  memcpy(id_out, &id, sizeof(id));
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_comm_init(cess_bls_ctx* c, int nranks, int rank, const uint8_t id_in[CESS_BLS_COMM_ID_BYTES]) {
+  ENTRY(c);
+  if (!c->subs.empty() || !id_in || nranks <= 0 || rank < 0 || rank >= nranks || c->comm) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  ncclUniqueId id;
+  memcpy(&id, id_in, sizeof(id));
+  ncclComm_t comm = nullptr;
+  NCCLCHK(ncclCommInitRank(&comm, nranks, id, rank));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return CESS_BLS_OK;
+}
+
+// all-gather `count` elements per rank in place: rank r's block at buf + r * count
+static int allgather_inplace(cess_bls_ctx* c, void* buf, size_t count, ncclDataType_t t, size_t esize, hipStream_t s) {
+  char* b = static_cast<char*>(buf);
+  NCCLCHK(ncclAllGather(b + (size_t)c->rank * count * esize, b, count, t, c->comm, s));
+  return CESS_BLS_OK;
+}
+
+extern "C" int cess_bls_verify_batch_sharded(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                             const uint8_t* msgs, const uint64_t* offs, uint8_t* codes_out,
+                                             uint64_t* bitmap_out) {
+  ENTRY(c);
+  if (!c->comm) return CESS_BLS_E_NO_COMM;
+  if (n && (!sigs || !pks || !offs)) return CESS_BLS_E_INVALID_ARG;
+  uint64_t b, e, wpr;
+  shard_of(n, c->nranks, c->rank, &b, &e, &wpr);
+  const uint64_t m = e - b;
+  // the rank's verdicts (host), then one in-place all-gather of words and codes
+  std::vector<uint8_t> codes(std::max<uint64_t>(wpr * 64, 1), 0xff);
+  std::vector<uint64_t> words(std::max<uint64_t>(wpr, 1), 0);
+  int r = CESS_BLS_OK;
+  if (m) r = verify_host(c, m, sigs + 48 * b, pks + 96 * b, msgs, offs + b, nullptr, codes.data(), words.data(), nullptr);
+  if (r) return r;
+  if (wpr == 0) return CESS_BLS_OK;   // empty batch
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  r = order_begin(c, s);
+  if (r) return r;
+  if (c->comm_words.ensure(c->nranks * wpr * 8) | c->comm_codes.ensure(c->nranks * wpr * 64)) return CESS_BLS_E_OOM;
+  uint64_t* dw = c->comm_words.as<uint64_t>();
+  uint8_t* dc = c->comm_codes.as<uint8_t>();
+  HIPCHK(hipMemcpyAsync(dw + c->rank * wpr, words.data(), wpr * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(dc + c->rank * wpr * 64, codes.data(), wpr * 64, hipMemcpyHostToDevice, s));
+  r = allgather_inplace(c, dw, wpr, ncclUint64, 8, s);
+  if (r) return r;
+  if (codes_out) {
+    r = allgather_inplace(c, dc, wpr * 64, ncclUint8, 1, s);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(codes_out, dc, n, hipMemcpyDeviceToHost, s));
+  }
+  if (bitmap_out) HIPCHK(hipMemcpyAsync(bitmap_out, dw, ((n + 63) / 64) * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return order_end(c, s);
+}
+
+extern "C" int cess_bls_verify_batch_sharded_device(cess_bls_ctx* c, size_t n_total, const uint8_t* d_sigs,
+                                                    const uint8_t* d_pks, const uint8_t* d_msgs,
+                                                    const uint64_t* d_offs, uint8_t* d_codes_all,
+                                                    uint64_t* d_bitmap_all, void* stream) {
+  ENTRY(c);
+  if (!c->comm) return CESS_BLS_E_NO_COMM;
+  if (!d_bitmap_all) return CESS_BLS_E_INVALID_ARG;
+  uint64_t b, e, wpr;
+  shard_of(n_total, c->nranks, c->rank, &b, &e, &wpr);
+  const uint64_t m = e - b;
+  if (m && (!d_sigs || !d_pks || !d_offs)) return CESS_BLS_E_INVALID_ARG;
+  if (wpr == 0) return CESS_BLS_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  int r = order_begin(c, s);
+  if (r) return r;
+  uint64_t* my_words = d_bitmap_all + c->rank * wpr;
+  uint8_t* codes = d_codes_all ? d_codes_all + c->rank * wpr * 64 : nullptr;
+  if (!codes) {
+    if (c->comm_codes.ensure(std::max<uint64_t>(m, 1))) return CESS_BLS_E_OOM;
+    codes = c->comm_codes.as<uint8_t>();
+  }
+  // words of the rank's run past its last record (a short or empty last shard)
+  const uint64_t used = (m + 63) / 64;
+  if (used < wpr) HIPCHK(hipMemsetAsync(my_words + used, 0, (wpr - used) * 8, s));
+  for (uint64_t off = 0; off < m; off += c->cap) {
+    const uint64_t q = std::min<uint64_t>(c->cap, m - off);
+    r = run_chunk(c, s, q, d_sigs + 48 * off, d_pks + 96 * off, d_msgs, d_offs + off, nullptr, codes + off,
+                  my_words + off / 64, nullptr);
+    if (r) return r;
+    if (c->flags & CESS_BLS_F_PROFILE) {
+      r = collect_profile(c, s);
+      if (r) return r;
+    }
+  }
+  r = allgather_inplace(c, d_bitmap_all, wpr, ncclUint64, 8, s);
+  if (r) return r;
+  if (d_codes_all) {
+    r = allgather_inplace(c, d_codes_all, wpr * 64, ncclUint8, 1, s);
+    if (r) return r;
+  }
+  return order_end(c, s);
+}
+
+extern "C" int cess_bls_verify_batch_rlc_sharded(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                                 const uint8_t* msgs, const uint64_t* offs, const uint8_t* seed32,
+                                                 uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4,
+                                                 int* global_ok_out) {
+  ENTRY(c);
+  if (!c->comm) return CESS_BLS_E_NO_COMM;
+  uint8_t gt[576];
+  int r = rlc_begin(c, n, sigs, pks, msgs, offs, seed32, gt);
+  if (r) return r;
+  // Gt partials: one 576-byte slot per rank, all-gathered in place, multiplied
+  // on the device (RCCL has no Fp12 reduction operator)
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  r = order_begin(c, s);
+  if (r) return r;
+  if (c->comm_buf.ensure((size_t)c->nranks * 576)) return CESS_BLS_E_OOM;
+  uint8_t* d = c->comm_buf.as<uint8_t>();
+  HIPCHK(hipMemcpyAsync(d + (size_t)c->rank * 576, gt, 576, hipMemcpyHostToDevice, s));
+  r = allgather_inplace(c, d, 576, ncclUint8, 1, s);
+  if (r) return r;
+  HIPCHK(hipStreamSynchronize(s));
+  r = order_end(c, s);
+  if (r) return r;
+  int one = 0;
+  r = gt_product_is_one(c, c->nranks, d, true, &one);
+  if (r) return r;
+  if (global_ok_out) *global_ok_out = one;
+  return rlc_finish(c, codes_out, bitmap_out, stats4);
+}
+
+extern "C" int cess_bls_comm_barrier(cess_bls_ctx* c) {
+  double v = 0;
+  return cess_bls_comm_max_f64(c, &v);
+}
+
+extern "C" int cess_bls_comm_max_f64(cess_bls_ctx* c, double* value) {
+  ENTRY(c);
+  if (!c->comm) return CESS_BLS_E_NO_COMM;
+  if (!value) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int r = order_begin(c, s);
+  if (r) return r;
+  if (c->comm_buf.ensure(std::max<size_t>(8, (size_t)c->nranks * 576))) return CESS_BLS_E_OOM;
+  double* d = c->comm_buf.as<double>();
+  HIPCHK(hipMemcpyAsync(d, value, 8, hipMemcpyHostToDevice, s));
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, c->comm, s));
+  HIPCHK(hipMemcpyAsync(value, d, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return order_end(c, s);
+}
+
+// ---------------------------------------------------------------------------
+// one process, several GPUs (cess_bls_config.n_devices > 1)
+// ---------------------------------------------------------------------------
+int cess_multi_create(const cess_bls_config* cfg, int ndev, cess_bls_ctx* c) {
+  const int nd = cfg->n_devices;
+  c->device = -1;
+  c->flags = cfg->flags;
+  c->mode = cfg->mode;
+  for (int k = 0; k < nd; k++) {
+    const int dev = cfg->devices ? cfg->devices[k] : k;
+    if (dev < 0 || dev >= ndev) return CESS_BLS_E_INVALID_ARG;
+    cess_bls_config sc = *cfg;
+    sc.device = dev;
+    sc.n_devices = 1;
+    sc.devices = nullptr;
+    cess_bls_ctx* s = nullptr;
+    int r = cess_bls_ctx_create(&sc, &s);
+    if (r) return r;
+    c->subs.push_back(s);
+  }
+  c->cap = c->subs[0]->cap;
+  return CESS_BLS_OK;
+}
+
+// Run f(sub, begin, end) for every sub-context's shard of n records on its own
+// host thread; shards are whole bitmap words (shard_of).  First failure wins.
+template <class F>
+static int for_each_shard(cess_bls_ctx* c, uint64_t n, F&& f) {
+  const int nd = (int)c->subs.size();
+  std::vector<int> st(nd, CESS_BLS_OK);
+  std::vector<std::thread> th;
+  for (int k = 0; k < nd; k++) {
+    uint64_t b, e;
+    shard_of(n, nd, k, &b, &e, nullptr);
+    if (e <= b) continue;
+    th.emplace_back([&, k, b, e] { st[k] = f(c->subs[k], b, e); });
+  }
+  for (auto& t : th) t.join();
+  for (int v : st)
+    if (v) return v;
+  return CESS_BLS_OK;
+}
+
+int cess_multi_verify(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                      const uint64_t* offs, uint8_t* codes_out, uint64_t* bitmap_out, bool rlc, const uint8_t* seed32,
+                      uint64_t* stats4) {
+  if (n == 0) return CESS_BLS_OK;
+  if (!sigs || !pks || !offs) return CESS_BLS_E_INVALID_ARG;
+  if (!rlc)
+    return for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+      return verify_host(s, e - b, sigs + 48 * b, pks + 96 * b, msgs, offs + b, nullptr,
+                         codes_out ? codes_out + b : nullptr, bitmap_out ? bitmap_out + b / 64 : nullptr, nullptr);
+    });
+  // RLC: every device checks its shard (distinct scalar index ranges), the Gt
+  // partials are multiplied on device 0 (the batch-level verdict, unused for
+  // the codes), and each device bisects iff its own check failed
+  const int nd = (int)c->subs.size();
+  std::vector<uint8_t> gts((size_t)nd * 576, 0);
+  std::vector<std::vector<uint64_t>> st(nd, std::vector<uint64_t>(4, 0));
+  uint8_t seed[32];
+  if (seed32) memcpy(seed, seed32, 32);
+  else if (os_random(seed, 32)) return CESS_BLS_E_INVALID_ARG;
+  for (int k = 0; k < nd; k++) gts[(size_t)k * 576 + 47] = 1;   // an empty shard's partial is one
+  // the device index goes into the scalar index (k << 40), as the rank does
+  // across processes, so no r_i is shared between shards under one seed
+  int r = for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    int k = 0;
+    while (c->subs[k] != s) k++;
+    return rlc_begin_at(s, e - b, sigs + 48 * b, pks + 96 * b, msgs, offs + b, seed, (uint64_t)k << 40,
+                        &gts[(size_t)k * 576]);
+  });
+  if (r) return r;
+  int one = 0;
+  r = gt_product_is_one(c->subs[0], nd, gts.data(), false, &one);
+  if (r) return r;
+  r = for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    int k = 0;
+    while (c->subs[k] != s) k++;
+    return rlc_finish(s, codes_out ? codes_out + b : nullptr, bitmap_out ? bitmap_out + b / 64 : nullptr,
+                      st[k].data());
+  });
+  if (r) return r;
+  if (stats4) {
+    for (int q = 0; q < 3; q++) {
+      stats4[q] = 0;
+      for (int k = 0; k < nd; k++) stats4[q] += st[k][q];
+    }
+    stats4[3] = 0;
+    for (int k = 0; k < nd; k++) stats4[3] = std::max(stats4[3], st[k][3]);
+  }
+  return CESS_BLS_OK;
+}
+
+int cess_multi_verify_var(cess_bls_ctx* c, size_t n, const uint8_t* sig_data, const uint64_t* sig_offsets,
+                          const uint8_t* pk_data, const uint64_t* pk_offsets, const uint8_t* msgs,
+                          const uint64_t* msg_offsets, uint8_t* codes_out, uint64_t* bitmap_out) {
+  if (n == 0) return CESS_BLS_OK;
+  if (!sig_offsets || !pk_offsets || !msg_offsets) return CESS_BLS_E_INVALID_ARG;
+  return for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    return verify_var_host(s, e - b, sig_data, sig_offsets + b, pk_data, pk_offsets + b, msgs, msg_offsets + b,
+                           codes_out ? codes_out + b : nullptr, bitmap_out ? bitmap_out + b / 64 : nullptr);
+  });
+}
+
+int cess_multi_keys_load(cess_bls_ctx* c, size_t k, const uint8_t* pks, uint8_t* key_codes_out) {
+  // the table is replicated on every device; codes from device 0
+  const int nd = (int)c->subs.size();
+  std::vector<int> st(nd, CESS_BLS_OK);
+  std::vector<std::thread> th;
+  for (int d = 0; d < nd; d++)
+    th.emplace_back([&, d] { st[d] = cess_keys_load_one(c->subs[d], k, pks, d == 0 ? key_codes_out : nullptr); });
+  for (auto& t : th) t.join();
+  for (int v : st)
+    if (v) return v;
+  return CESS_BLS_OK;
+}
+
+int cess_multi_keyed(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint32_t* key_idx, const uint8_t* msgs,
+                     const uint64_t* offs, uint8_t* codes_out, uint64_t* bitmap_out) {
+  if (n == 0) return CESS_BLS_OK;
+  if (!sigs || !key_idx || !offs) return CESS_BLS_E_INVALID_ARG;
+  return for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    return cess_keyed_one(s, e - b, sigs + 48 * b, key_idx + b, msgs, offs + b, codes_out ? codes_out + b : nullptr,
+                          bitmap_out ? bitmap_out + b / 64 : nullptr);
+  });
+}
+
+int cess_multi_gen(cess_bls_ctx* c, int kind, size_t n, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs,
+                   uint8_t* out) {
+  if (n == 0) return CESS_BLS_OK;
+  const size_t ob = kind == 0 ? 96 : 48;
+  return for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    return cess_gen_one(s, kind, e - b, sks ? sks + 32 * b : nullptr, msgs, offs ? offs + b : nullptr, out + ob * b);
+  });
+}
+
+int cess_multi_gt(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                  const uint64_t* offs, uint8_t* codes_out, uint8_t* gt_out) {
+  if (n == 0) return CESS_BLS_OK;
+  if (!sigs || !pks || !offs) return CESS_BLS_E_INVALID_ARG;
+  return for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    return verify_host(s, e - b, sigs + 48 * b, pks + 96 * b, msgs, offs + b, nullptr,
+                       codes_out ? codes_out + b : nullptr, nullptr, gt_out + 576 * b);
+  });
+}

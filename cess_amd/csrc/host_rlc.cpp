@@ -1,0 +1,473 @@
+// RLC batch mode (north_star "optional random-linear-combination batch mode";
+// SURVEY §8(d) C4, §8(e)).  One random linear combination per (sub)batch; on
+// failure the batch is bisected down to leaves of kRlcLeaf records, which are
+// verified per signature, so the final codes are those of
+// cess_bls_verify_batch (up to the 2^-127 soundness error per check).
+#include <sys/random.h>
+
+#include "host.hpp"
+
+using namespace cess_host;
+
+namespace {
+constexpr uint64_t kRlcLeaf = 2048;   // records verified per signature
+constexpr uint64_t kRlcFan = 16;      // bisection fan-out per level
+constexpr uint64_t kProdLanes = 64;   // lanes per range in the Fp12 segment product
+
+// one (range, key group) term of a batched check: perm positions [lo, hi)
+struct Term {
+  uint32_t range, group;
+  uint64_t lo, hi;
+};
+}  // namespace
+
+int cess_host::os_random(uint8_t* out, size_t n) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = getrandom(out + got, n - got, 0);
+    if (r <= 0) return CESS_BLS_E_INVALID_ARG;
+    got += (size_t)r;
+  }
+  return CESS_BLS_OK;
+}
+
+// Segmented sums: out[s] (stride out_stride) = sum of in[perm[off_s + j]], j < cnt_s.
+// Two passes of k_g1_sum_segs (B partial sums per segment, then one).
+static int rlc_sums(RlcState& R, hipStream_t s, const std::vector<uint64_t>& off, const std::vector<uint64_t>& cnt,
+                    const uint32_t* in, uint64_t in_stride, uint32_t* out, uint64_t out_stride) {
+  const uint64_t ns = off.size();
+  if (ns == 0) return CESS_BLS_OK;
+  uint64_t mx = 1;
+  for (uint64_t v : cnt) mx = std::max(mx, v);
+  const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(1, 1024 / ns), (mx + 255) / 256));
+  std::vector<uint64_t> h(4 * ns);
+  for (uint64_t q = 0; q < ns; q++) h[q] = off[q], h[ns + q] = cnt[q], h[2 * ns + q] = q * B, h[3 * ns + q] = B;
+  if (B * ns >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
+  if (R.seg.ensure(h.size() * 8) || R.part.ensure(ns * B * 36 * 4)) return CESS_BLS_E_OOM;
+  HIPCHK(hipMemcpyAsync(R.seg.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+  const uint64_t* d = R.seg.as<uint64_t>();
+  hipLaunchKernelGGL(k_g1_sum_segs, dim3((unsigned)(B * ns)), dim3(256), 0, s, (uint32_t)B, d, d + ns,
+                     (const uint32_t*)R.d_perm.as<uint32_t>(), in, in_stride, R.part.as<uint32_t>(), ns * B);
+  hipLaunchKernelGGL(k_g1_sum_segs, dim3((unsigned)ns), dim3(256), 0, s, 1u, d + 2 * ns, d + 3 * ns,
+                     (const uint32_t*)nullptr, (const uint32_t*)R.part.as<uint32_t>(), ns * B, out, out_stride);
+  HIPCHK(hipGetLastError());
+  // the host vector h must outlive the async copy
+  HIPCHK(hipStreamSynchronize(s));
+  return CESS_BLS_OK;
+}
+
+// RLC checks of NR perm-position ranges in one batch: ok[r] = the product of
+// range r's pairings is 1.  Only the (range, key group) terms that intersect
+// are formed (perm is sorted by group, so a range meets a contiguous run of
+// groups): at most NR + K + NR terms per batch, never NR * K.  gt_out
+// (optional, NR == 1): the Gt value of the check.
+static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
+                           std::vector<uint8_t>& ok, uint8_t* gt_out) {
+  hipStream_t s = c->stream;
+  const uint64_t NR = rg.size();
+  R.checks += NR;
+  std::vector<Term> terms;
+  std::vector<uint64_t> so(NR), sc(NR), tbeg(NR + 1, 0);
+  for (uint64_t r = 0; r < NR; r++) {
+    const uint64_t a = rg[r].first, b = rg[r].second;
+    so[r] = a, sc[r] = b - a;
+    tbeg[r] = terms.size();
+    if (b > a) {
+      // first group with gbeg[g + 1] > a
+      uint64_t g = std::upper_bound(R.gbeg.begin(), R.gbeg.end(), a) - R.gbeg.begin() - 1;
+      for (; g < R.K && R.gbeg[g] < b; g++) {
+        const uint64_t lo = std::max(a, R.gbeg[g]), hi = std::min(b, R.gbeg[g + 1]);
+        if (hi > lo) terms.push_back({(uint32_t)r, (uint32_t)g, lo, hi});
+      }
+    }
+  }
+  tbeg[NR] = terms.size();
+  const uint64_t M = terms.size();
+  ok.assign(NR, 1);
+  if (M == 0) {
+    if (gt_out) {
+      memset(gt_out, 0, 576);
+      gt_out[47] = 1;
+    }
+    return CESS_BLS_OK;
+  }
+  if (M >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
+  int r = 0;
+  r |= R.S.ensure(NR * 36 * 4) | R.Qs.ensure(M * 36 * 4);
+  r |= R.rec_code.ensure(M) | R.rec_inf.ensure(M) | R.rec_sig.ensure(M * CESS_W_G1 * 4);
+  r |= R.rec_h.ensure(M * CESS_W_G1 * 4) | R.rec_f.ensure(M * CESS_W_FP12 * 4) | R.rec_f2.ensure(M * CESS_W_FP12 * 4);
+  r |= R.acc.ensure(NR * CESS_W_FP12 * 4) | R.slots.ensure(NR * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
+  r |= R.part2.ensure(NR * kProdLanes * CESS_W_FP12 * 4);
+  r |= R.fin_code.ensure(NR) | R.fin_bm.ensure(((NR + 63) / 64) * 8) | R.gt.ensure(NR * 576);
+  r |= R.lists.ensure((2 * M + NR + 1) * 4);
+  if (r) return CESS_BLS_E_OOM;
+  std::vector<uint64_t> qo(M), qc(M);
+  std::vector<uint32_t> lists(2 * M + NR + 1);
+  for (uint64_t j = 0; j < M; j++) {
+    qo[j] = terms[j].lo, qc[j] = terms[j].hi - terms[j].lo;
+    lists[j] = terms[j].range;
+    lists[M + j] = terms[j].group;
+  }
+  for (uint64_t q = 0; q <= NR; q++) lists[2 * M + q] = (uint32_t)tbeg[q];
+  HIPCHK(hipMemcpyAsync(R.lists.p, lists.data(), lists.size() * 4, hipMemcpyHostToDevice, s));
+  const uint32_t* d_range = R.lists.as<uint32_t>();
+  const uint32_t* d_group = d_range + M;
+  const uint32_t* d_tbeg = d_range + 2 * M;
+  r = rlc_sums(R, s, so, sc, R.P.as<uint32_t>(), R.n, R.S.as<uint32_t>(), NR);
+  if (r) return r;
+  r = rlc_sums(R, s, qo, qc, R.Q.as<uint32_t>(), R.n, R.Qs.as<uint32_t>(), M);
+  if (r) return r;
+  hipLaunchKernelGGL(k_rlc_pairs_list, dim3((unsigned)((M + 63) / 64)), dim3(64), 0, s, (uint32_t)M, (uint32_t)NR, d_range, d_group,
+                     (const uint32_t*)R.S.as<uint32_t>(), (const uint8_t*)R.pk_usable.as<uint8_t>(),
+                     R.rec_code.as<uint8_t>(), R.rec_inf.as<uint8_t>(), R.rec_sig.as<uint32_t>(),
+                     R.rec_h.as<uint32_t>(), R.Qs.as<uint32_t>());
+  // the Miller loop reads each term's key rows straight from the distinct-key
+  // table (cidx = group, table stride K): nothing is replicated
+  hipLaunchKernelGGL(k_miller, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, M,
+                     (const uint8_t*)R.rec_code.as<uint8_t>(), (const uint8_t*)R.rec_inf.as<uint8_t>(),
+                     (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
+                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)R.pk_coeffs.as<uint4>(),
+                     R.rec_f.as<uint4>(), R.rec_f2.as<uint4>(), M, d_group, (uint64_t)R.K);
+  hipLaunchKernelGGL(k_fp12_prod_segs, dim3((unsigned)NR), dim3((unsigned)kProdLanes), 0, s, (uint32_t)NR, d_tbeg,
+                     (const uint4*)R.rec_f.as<uint4>(), (uint64_t)M, R.part2.as<uint4>(), R.acc.as<uint4>());
+  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
+  hipLaunchKernelGGL(k_final, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
+                     R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(), gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
+  HIPCHK(hipGetLastError());
+  std::vector<uint8_t> codes(NR);
+  HIPCHK(hipMemcpyAsync(codes.data(), R.fin_code.p, NR, hipMemcpyDeviceToHost, s));
+  if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint64_t q = 0; q < NR; q++) ok[q] = codes[q] == CODE_OK;
+  return CESS_BLS_OK;
+}
+
+// rlc_begin with an index base for the scalars (ranks pass rank << 40, so no
+// r_i is shared across shards under one seed)
+int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                        const uint64_t* offs, const uint8_t* seed_in, uint64_t index_hi, uint8_t* gt_out) {
+  if (n && (!sigs || !pks || !offs || (!msgs && offs[n] != offs[0]))) return CESS_BLS_E_INVALID_ARG;
+  if (n >= (1ull << 32)) return CESS_BLS_E_INVALID_ARG;
+  uint8_t seed32[32];
+  if (seed_in) memcpy(seed32, seed_in, 32);
+  else if (os_random(seed32, 32)) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->rlc) c->rlc = new RlcState();
+  RlcState& R = *c->rlc;
+  R.n = n, R.sigs = sigs, R.pks = pks, R.msgs = msgs, R.offs = offs;
+  R.checks = R.leaves = R.leaf_sigs = 0;
+  R.codes.assign(n, 0);
+  R.local_ok = true;
+  R.per_sig = false;
+  R.K = 0;
+  auto gt_one = [&]() {
+    if (gt_out) {   // the empty product: Gt one
+      memset(gt_out, 0, 576);
+      gt_out[47] = 1;
+    }
+  };
+  if (n == 0) {
+    gt_one();
+    return CESS_BLS_OK;
+  }
+  hipStream_t s = c->stream;
+  int r = order_begin(c, s);
+  if (r) return r;
+  // 1. key groups (dedup of the 96-byte encodings; open addressing on a
+  //    64-bit hash, full compare) and a counting sort by group
+  std::vector<uint32_t> grp(n);
+  std::vector<uint64_t> first;
+  {
+    auto khash = [](const uint8_t* k) {
+      uint64_t h = 0x9E3779B97F4A7C15ull;
+      for (int q = 0; q < 96; q += 8) {
+        uint64_t w;
+        memcpy(&w, k + q, 8);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+      }
+      return h;
+    };
+    std::vector<uint32_t> slot(64, 0);   // group id + 1; 0 = empty
+    uint64_t mask = 63;
+    for (uint64_t i = 0; i < n; i++) {
+      const uint8_t* k = pks + 96 * i;
+      uint64_t h = khash(k) & mask;
+      while (slot[h] && memcmp(pks + 96 * first[slot[h] - 1], k, 96) != 0) h = (h + 1) & mask;
+      if (!slot[h]) {
+        first.push_back(i);
+        slot[h] = (uint32_t)first.size();
+        if (2 * first.size() > mask) {   // grow and rehash
+          std::vector<uint32_t> ns(2 * (mask + 1), 0);
+          const uint64_t nm = 2 * (mask + 1) - 1;
+          for (uint32_t g = 0; g < first.size(); g++) {
+            uint64_t q = khash(pks + 96 * first[g]) & nm;
+            while (ns[q]) q = (q + 1) & nm;
+            ns[q] = g + 1;
+          }
+          slot.swap(ns);
+          mask = nm;
+        }
+        grp[i] = (uint32_t)first.size() - 1;
+      } else {
+        grp[i] = slot[h] - 1;
+      }
+    }
+  }
+  const uint32_t K = R.K = (uint32_t)first.size();
+  // 1b. many distinct keys: a combination needs K + 1 pairings anyway and a
+  //     forgery's bisection would cost more than per-signature verification,
+  //     so the shard is verified per signature (exact codes, Gt partial one)
+  if (8 * (uint64_t)K > n) {
+    R.per_sig = true;
+    r = verify_host(c, n, sigs, pks, msgs, offs, nullptr, R.codes.data(), nullptr, nullptr);
+    if (r) return r;
+    R.leaf_sigs = n;
+    gt_one();
+    return CESS_BLS_OK;
+  }
+  R.gbeg.assign(K + 1, 0);
+  for (uint64_t i = 0; i < n; i++) R.gbeg[grp[i] + 1]++;
+  for (uint32_t g = 0; g < K; g++) R.gbeg[g + 1] += R.gbeg[g];
+  R.perm.resize(n);
+  {
+    std::vector<uint64_t> pos(R.gbeg.begin(), R.gbeg.end() - 1);
+    for (uint64_t i = 0; i < n; i++) R.perm[pos[grp[i]]++] = (uint32_t)i;
+  }
+  // 2. device buffers
+  r = 0;
+  r |= R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4) | R.d_perm.ensure(n * 4) | R.d_seed.ensure(32);
+  r |= R.pk_in.ensure((uint64_t)K * 96);
+  r |= R.pk_code.ensure(K) | R.pk_inf.ensure(K) | R.pk_aff.ensure((uint64_t)K * CESS_W_G2 * 4);
+  r |= R.pk_coeffs.ensure((uint64_t)K * CESS_W_COEFFS * 4) | R.pk_usable.ensure(K);
+  if (r) return CESS_BLS_E_OOM;
+  {
+    uint32_t sw[8];
+    for (int w = 0; w < 8; w++)
+      sw[w] = ((uint32_t)seed32[4 * w] << 24) | ((uint32_t)seed32[4 * w + 1] << 16) | ((uint32_t)seed32[4 * w + 2] << 8) |
+              seed32[4 * w + 3];
+    HIPCHK(hipMemcpyAsync(R.d_seed.p, sw, 32, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));   // sw is a stack buffer
+  }
+  HIPCHK(hipMemcpyAsync(R.d_perm.p, R.perm.data(), n * 4, hipMemcpyHostToDevice, s));
+  // 3. distinct keys: decode (G2Affine::from_compressed, src/lib.rs:74) + G2Prepared (:88), once per key
+  std::vector<uint8_t> kbytes((uint64_t)K * 96), pkc(K), pki(K), usable(K);
+  for (uint32_t g = 0; g < K; g++) memcpy(&kbytes[96 * (uint64_t)g], pks + 96 * first[g], 96);
+  const uint32_t strict = (c->flags & CESS_BLS_F_STRICT_IDENTITY) ? 1u : 0u;
+  HIPCHK(hipMemcpyAsync(R.pk_in.p, kbytes.data(), kbytes.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(R.pk_code.p, 0, K, s));
+  HIPCHK(hipMemsetAsync(R.pk_inf.p, 0, K, s));
+  hipLaunchKernelGGL(k_decode_pk, dim3(grid_for(K)), dim3(kBlock), 0, s, (uint64_t)K, R.pk_in.as<uint8_t>(),
+                     (const uint8_t*)nullptr, R.pk_code.as<uint8_t>(), R.pk_inf.as<uint8_t>(), R.pk_aff.as<uint32_t>(),
+                     (uint64_t)K, strict);
+  hipLaunchKernelGGL(k_prepare, dim3(grid_for(K)), dim3(kBlock), 0, s, (uint64_t)K,
+                     (const uint32_t*)R.pk_aff.as<uint32_t>(), R.pk_coeffs.as<uint4>(), (uint64_t)K);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(pkc.data(), R.pk_code.p, K, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(pki.data(), R.pk_inf.p, K, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint32_t g = 0; g < K; g++) usable[g] = pkc[g] == 0 && !(pki[g] & INF_PK);
+  HIPCHK(hipMemcpyAsync(R.pk_usable.p, usable.data(), K, hipMemcpyHostToDevice, s));
+  // 4. per chunk: decode sig (src/lib.rs:144), key codes in reference precedence
+  //    (signature first, :244-245), hash_to_g1 (:25-31), P_i = r_i sig_i, Q_i = r_i H_i
+  std::vector<uint8_t> hc, hi;
+  std::vector<uint64_t> rebased;
+  for (uint64_t off = 0; off < n; off += c->cap) {
+    const uint64_t m = std::min<uint64_t>(c->cap, n - off);
+    const uint64_t mb0 = offs[off], mb1 = offs[off + m];
+    if (mb1 < mb0) return CESS_BLS_E_INVALID_ARG;
+    rebased.resize(m + 1);
+    for (uint64_t j = 0; j <= m; j++) {
+      if (j && offs[off + j] < offs[off + j - 1]) return CESS_BLS_E_INVALID_ARG;
+      rebased[j] = offs[off + j] - mb0;
+    }
+    r = c->in_sigs.ensure(m * 48) | c->in_msgs.ensure(std::max<uint64_t>(mb1 - mb0, 1)) | c->in_offs.ensure((m + 1) * 8);
+    if (r) return CESS_BLS_E_OOM;
+    HIPCHK(hipMemcpyAsync(c->in_sigs.p, sigs + 48 * off, m * 48, hipMemcpyHostToDevice, s));
+    if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+    const unsigned g = grid_for(m);
+    hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
+                       c->code.as<uint8_t>(), c->inf.as<uint8_t>(), c->sig_aff.as<uint32_t>(), c->cap);
+    HIPCHK(hipGetLastError());
+    hc.resize(m);
+    hi.resize(m);
+    HIPCHK(hipMemcpyAsync(hc.data(), c->code.p, m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hi.data(), c->inf.p, m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (uint64_t j = 0; j < m; j++) {
+      if (hc[j] != 0) continue;
+      const uint32_t gg = grp[off + j];
+      if (pkc[gg] != 0) hc[j] = pkc[gg];
+      else if (pki[gg] & INF_PK) hi[j] |= INF_PK;
+    }
+    memcpy(&R.codes[off], hc.data(), m);
+    HIPCHK(hipMemcpyAsync(c->code.p, hc.data(), m, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->inf.p, hi.data(), m, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
+                       (const uint8_t*)c->code.as<uint8_t>(), c->h_aff.as<uint32_t>(), c->cap);
+    hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)c->code.as<uint8_t>(),
+                       (const uint8_t*)c->inf.as<uint8_t>(), (const uint32_t*)c->sig_aff.as<uint32_t>(),
+                       (const uint32_t*)c->h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(),
+                       index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->cap, (uint64_t)n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // hc/hi are reused by the next chunk
+  }
+  // 5. the batch check (this shard's Gt partial)
+  std::vector<uint8_t> ok;
+  r = rlc_check_multi(c, R, {{0, n}}, ok, gt_out);
+  if (r) return r;
+  R.local_ok = ok[0] != 0;
+  return order_end(c, s);
+}
+
+int cess_host::rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                         const uint64_t* offs, const uint8_t* seed32, uint8_t* gt_out) {
+  const uint64_t hi = c->comm ? ((uint64_t)c->rank << 40) : 0;
+  return rlc_begin_at(c, n, sigs, pks, msgs, offs, seed32, hi, gt_out);
+}
+
+int cess_host::gt_product_is_one(cess_bls_ctx* c, size_t m, const uint8_t* gts, bool on_device, int* is_one) {
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->rlc) c->rlc = new RlcState();
+  RlcState& R = *c->rlc;
+  if (m == 0) {
+    *is_one = 1;
+    return CESS_BLS_OK;
+  }
+  hipStream_t s = c->stream;
+  int r = order_begin(c, s);
+  if (r) return r;
+  if (R.gts.ensure(m * 576) | R.tmp.ensure(2 * CESS_W_FP12 * 4) | R.fin_code.ensure(1)) return CESS_BLS_E_OOM;
+  const uint8_t* d_gts = gts;
+  if (!on_device) {
+    HIPCHK(hipMemcpyAsync(R.gts.p, gts, m * 576, hipMemcpyHostToDevice, s));
+    d_gts = R.gts.as<uint8_t>();
+  }
+  hipLaunchKernelGGL(k_gt_prod, dim3(1), dim3(64), 0, s, (uint32_t)m, d_gts, R.tmp.as<uint4>(), R.fin_code.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  uint8_t code = 0xff;
+  HIPCHK(hipMemcpyAsync(&code, R.fin_code.p, 1, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *is_one = code == CODE_OK;
+  return order_end(c, s);
+}
+
+// Bisect iff this shard's own check failed: honest records contribute exactly
+// one to the shard's partial, so a failed local check proves an invalid member,
+// and no other shard's partial may cancel that proof.
+int cess_host::rlc_finish(cess_bls_ctx* c, uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4) {
+  if (!c->rlc) return CESS_BLS_E_INVALID_ARG;
+  RlcState& R = *c->rlc;
+  const uint64_t n = R.n;
+  std::vector<uint8_t>& codes = R.codes;
+  if (!R.per_sig && !R.local_ok) {
+    // batched bisection over perm positions: every failing range is split
+    // into up to kRlcFan parts, all parts of a level are checked in one batch;
+    // ranges of <= kRlcLeaf records are verified per signature (exact codes)
+    std::vector<std::pair<uint64_t, uint64_t>> level = {{0, n}}, parts, leaves;
+    std::vector<uint8_t> ok;
+    while (!level.empty()) {
+      parts.clear();
+      for (auto& w : level) {
+        const uint64_t len = w.second - w.first;
+        if (len <= kRlcLeaf) {
+          leaves.push_back(w);
+          continue;
+        }
+        const uint64_t fan = std::min<uint64_t>(kRlcFan, (len + kRlcLeaf - 1) / kRlcLeaf);
+        for (uint64_t q = 0; q < fan; q++) parts.push_back({w.first + len * q / fan, w.first + len * (q + 1) / fan});
+      }
+      level.clear();
+      if (!parts.empty()) {
+        int r = rlc_check_multi(c, R, parts, ok, nullptr);
+        if (r) return r;
+        for (size_t q = 0; q < parts.size(); q++)
+          if (!ok[q]) level.push_back(parts[q]);
+      }
+    }
+    // leaves: one per-signature batch over all their candidate records
+    std::vector<uint64_t> li, lo = {0};
+    std::vector<uint8_t> ls, lp, lm, lc;
+    for (auto& w : leaves) {
+      for (uint64_t j = w.first; j < w.second; j++)
+        if (codes[R.perm[j]] == 0) li.push_back(R.perm[j]);
+      R.leaves++;
+    }
+    const uint64_t m = li.size();
+    if (m) {
+      ls.resize(m * 48);
+      lp.resize(m * 96);
+      for (uint64_t q = 0; q < m; q++) {
+        const uint64_t i = li[q];
+        memcpy(&ls[48 * q], R.sigs + 48 * i, 48);
+        memcpy(&lp[96 * q], R.pks + 96 * i, 96);
+        lm.insert(lm.end(), R.msgs + R.offs[i], R.msgs + R.offs[i + 1]);
+        lo.push_back(lm.size());
+      }
+      lc.resize(m);
+      int r = verify_host(c, m, ls.data(), lp.data(), lm.empty() ? nullptr : lm.data(), lo.data(), nullptr, lc.data(),
+                          nullptr, nullptr);
+      if (r) return r;
+      for (uint64_t q = 0; q < m; q++) codes[li[q]] = lc[q];
+      R.leaf_sigs += m;
+    }
+  }
+  if (codes_out) memcpy(codes_out, codes.data(), n);
+  if (bitmap_out) bitmap_from_codes(codes.data(), n, bitmap_out);
+  if (stats4) {
+    stats4[0] = R.checks;
+    stats4[1] = R.leaves;
+    stats4[2] = R.leaf_sigs;
+    stats4[3] = R.K;
+  }
+  return CESS_BLS_OK;
+}
+
+int cess_host::verify_rlc_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                               const uint64_t* offs, const uint8_t* seed32, uint8_t* codes_out, uint64_t* bitmap_out,
+                               uint64_t* stats4) {
+  int r = rlc_begin_at(c, n, sigs, pks, msgs, offs, seed32, 0, nullptr);
+  if (r) return r;
+  return rlc_finish(c, codes_out, bitmap_out, stats4);
+}
+
+#define ENTRY(c)                          \
+  if (!(c)) return CESS_BLS_E_INVALID_ARG; \
+  CtxLock lock_(c);                        \
+  if (!lock_.ok()) return CESS_BLS_E_BUSY
+
+int cess_multi_verify(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                      const uint64_t* offs, uint8_t* codes_out, uint64_t* bitmap_out, bool rlc, const uint8_t* seed32,
+                      uint64_t* stats4);
+
+extern "C" int cess_bls_rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                  const uint8_t* msgs, const uint64_t* offs, const uint8_t* seed32, uint8_t* gt_out) {
+  ENTRY(c);
+  if (!c->subs.empty()) return CESS_BLS_E_INVALID_ARG;
+  return rlc_begin(c, n, sigs, pks, msgs, offs, seed32, gt_out);
+}
+
+extern "C" int cess_bls_gt_product_is_one(cess_bls_ctx* c, size_t m, const uint8_t* gts, int* is_one) {
+  ENTRY(c);
+  if (!is_one || (m && !gts)) return CESS_BLS_E_INVALID_ARG;
+  cess_bls_ctx* d = c->subs.empty() ? c : c->subs[0];
+  return gt_product_is_one(d, m, gts, false, is_one);
+}
+
+extern "C" int cess_bls_rlc_finish(cess_bls_ctx* c, int global_ok, uint8_t* codes_out, uint64_t* bitmap_out,
+                                   uint64_t* stats4) {
+  ENTRY(c);
+  (void)global_ok;   // a batch-level summary only; see rlc_finish
+  if (!c->subs.empty()) return CESS_BLS_E_INVALID_ARG;
+  return rlc_finish(c, codes_out, bitmap_out, stats4);
+}
+
+extern "C" int cess_bls_verify_batch_rlc(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                         const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
+                                         uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4) {
+  ENTRY(c);
+  if (!c->subs.empty())
+    return cess_multi_verify(c, n, sigs, pks, msgs, msg_offsets, codes_out, bitmap_out, true, seed32, stats4);
+  return verify_rlc_host(c, n, sigs, pks, msgs, msg_offsets, seed32, codes_out, bitmap_out, stats4);
+}

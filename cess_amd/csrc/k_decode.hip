@@ -39,7 +39,7 @@ __global__ CESS_LB void k_decode_sig(uint64_t n, const uint8_t* __restrict__ sig
 __global__ CESS_LB void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
                                                     const uint8_t* __restrict__ pre, uint8_t* __restrict__ code,
                                                     uint8_t* __restrict__ inf, uint32_t* __restrict__ pk_aff,
-                                                    uint64_t stride) {
+                                                    uint64_t stride, uint32_t strict_identity) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t pc = pre ? pre[i] : 0;
@@ -59,8 +59,14 @@ __global__ CESS_LB void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
       for (int k = 0; k < 24; k++) w[k] = bswap(src[k]);
       g2a d;
       if (!g2_decompress(w, d)) c = CODE_PK_POINT;
-      else if (d.inf) f |= INF_PK;
-      else q = d;
+      else if (d.inf) {
+        // the reference accepts the identity key (src/lib.rs:68-82); the
+        // optional strict mode rejects it as KeyValidate does
+        if (strict_identity) c = CODE_PK_POINT;
+        else f |= INF_PK;
+      } else {
+        q = d;
+      }
     }
   }
   // identity / rejected keys keep the generator so k_prepare stays well-defined
@@ -73,14 +79,20 @@ __global__ CESS_LB void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
 // keyed batch (cess_bls_verify_batch_keyed*): per-signature key verdicts taken
 // from the distinct-key table in the reference's precedence -- a bad signature
 // code stands, else the key's code, else the key's identity flag
-// (src/lib.rs:244-245)
-__global__ CESS_LB void k_merge_pk(uint64_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ key_code,
-                                   const uint8_t* __restrict__ key_inf, uint8_t* __restrict__ code,
-                                   uint8_t* __restrict__ inf) {
+// (src/lib.rs:244-245).  An index past the table (device-resident callers
+// pass unchecked indices) names no key: the record is rejected as PK_POINT
+// and k_miller, which skips records with a nonzero code, never reads its row.
+__global__ CESS_LB void k_merge_pk(uint64_t n, const uint32_t* __restrict__ idx, uint32_t nkeys,
+                                   const uint8_t* __restrict__ key_code, const uint8_t* __restrict__ key_inf,
+                                   uint8_t* __restrict__ code, uint8_t* __restrict__ inf) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (code[i] != 0) return;
   const uint32_t j = idx[i];
+  if (j >= nkeys) {
+    code[i] = CODE_PK_POINT;
+    return;
+  }
   const uint8_t kc = key_code[j];
   if (kc != 0) code[i] = kc;
   else inf[i] |= key_inf[j] & INF_PK;

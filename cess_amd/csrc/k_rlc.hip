@@ -9,10 +9,10 @@
 // Malformed encodings never enter the sums: they keep their decode codes.
 //
 // k_rlc_scale  : P_i = r_i sig_i, Q_i = r_i H(m_i)   (r_i = SHA-256(seed || i)[0:16] | 1)
-// k_g1_sum     : sum of projective G1 points over a (permuted) index range
-// k_rlc_pairs  : K+1 summed points -> affine Miller-loop records (k_miller input)
-// k_fp12_prod  : product of m Miller-loop values (one lane)
-// k_gt_prod    : product of m canonical Gt values == 1 ?  (cross-rank combine)
+// k_g1_sum_segs    : segmented sums of projective G1 points over permuted index ranges
+// k_rlc_pairs_list : (range, key group) terms -> affine Miller-loop records (k_miller input)
+// k_fp12_prod_segs : per-range product of the terms' Miller-loop values
+// k_gt_prod        : product of m canonical Gt values == 1 ?  (cross-rank combine)
 #include <hip/hip_runtime.h>
 #include "soa.hpp"
 
@@ -93,16 +93,22 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   st_g1p(Q, out_stride, i, q);
 }
 
-// out[blockIdx.x] = sum_{j < cnt} in[idx(j)], idx(j) = perm ? perm[off + j] : off + j
-__global__ __launch_bounds__(256, 1) void k_g1_sum(uint64_t cnt, const uint32_t* __restrict__ perm, uint64_t off,
-                                                   const uint32_t* __restrict__ in, uint64_t in_stride,
-                                                   uint32_t* __restrict__ out, uint64_t out_stride) {
+// Segmented sums (batched bisection): segment q = perm positions
+// [seg_off[q], seg_off[q] + seg_cnt[q]), B blocks per segment; block b =
+// q * B + bx writes out[b] (SoA stride out_stride).  With perm = nullptr the
+// positions index `in` directly (second pass over the partial sums).  1-D grid,
+// so the segment count is not bound by gridDim.y.
+__global__ __launch_bounds__(256, 1) void k_g1_sum_segs(uint32_t B, const uint64_t* __restrict__ seg_off,
+                                                        const uint64_t* __restrict__ seg_cnt,
+                                                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ in,
+                                                        uint64_t in_stride, uint32_t* __restrict__ out,
+                                                        uint64_t out_stride) {
   __shared__ uint32_t L[36][256];
-  const uint32_t t = threadIdx.x;
-  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t t = threadIdx.x, sg = blockIdx.x / B, bx = blockIdx.x % B;
+  const uint64_t T = (uint64_t)B * blockDim.x, off = seg_off[sg], cnt = seg_cnt[sg];
   g1p acc = proj_identity<fp>();
 #pragma unroll 1
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + t; j < cnt; j += T) {
+  for (uint64_t j = (uint64_t)bx * blockDim.x + t; j < cnt; j += T) {
     const uint64_t idx = perm ? perm[off + j] : off + j;
     acc = proj_add(acc, ld_g1p(in, in_stride, (uint32_t)idx));
   }
@@ -130,121 +136,60 @@ __global__ __launch_bounds__(256, 1) void k_g1_sum(uint64_t cnt, const uint32_t*
   if (t == 0) st_g1p(out, out_stride, blockIdx.x, acc);
 }
 
-// Segmented form (batched bisection): segment s = perm positions
-// [seg_off[s], seg_off[s] + seg_cnt[s]); grid (B, nseg); block (bx, s) writes
-// out[s * B + bx] (SoA stride out_stride).  With perm = nullptr the positions
-// index `in` directly (second pass over the partial sums).
-__global__ __launch_bounds__(256, 1) void k_g1_sum_segs(const uint64_t* __restrict__ seg_off,
-                                                        const uint64_t* __restrict__ seg_cnt,
-                                                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ in,
-                                                        uint64_t in_stride, uint32_t* __restrict__ out,
-                                                        uint64_t out_stride) {
-  __shared__ uint32_t L[36][256];
-  const uint32_t t = threadIdx.x, sg = blockIdx.y;
-  const uint64_t T = (uint64_t)gridDim.x * blockDim.x, off = seg_off[sg], cnt = seg_cnt[sg];
-  g1p acc = proj_identity<fp>();
-#pragma unroll 1
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + t; j < cnt; j += T) {
-    const uint64_t idx = perm ? perm[off + j] : off + j;
-    acc = proj_add(acc, ld_g1p(in, in_stride, (uint32_t)idx));
-  }
-#pragma unroll 1
-  for (uint32_t s = 128; s >= 1; s >>= 1) {
-    if (t >= s && t < 2 * s) {
-      const fp* e = &acc.x;
-#pragma unroll
-      for (int w = 0; w < 3; w++)
-#pragma unroll
-        for (int l = 0; l < 12; l++) L[12 * w + l][t - s] = e[w].v[l];
-    }
-    __syncthreads();
-    if (t < s) {
-      g1p o;
-      fp* e = &o.x;
-#pragma unroll
-      for (int w = 0; w < 3; w++)
-#pragma unroll
-        for (int l = 0; l < 12; l++) e[w].v[l] = L[12 * w + l][t];
-      acc = proj_add(acc, o);
-    }
-    __syncthreads();
-  }
-  if (t == 0) st_g1p(out, out_stride, sg * gridDim.x + blockIdx.x, acc);
-}
-
-// Batched check records: record j = r*K + g of range r (R ranges): pair 0 =
-// (S_r, -G2) on g == 0 only, pair 1 = (Q_{r,g}, pk_g).  Sums: S (stride R, r),
-// Qs (stride R*K, j).  Output in k_miller's SoA format (stride R*K).
-__global__ void k_rlc_pairs_multi(uint32_t R, uint32_t K, const uint32_t* __restrict__ S,
-                                  const uint32_t* __restrict__ Qs, const uint8_t* __restrict__ pk_usable,
-                                  uint8_t* __restrict__ code, uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff,
-                                  uint32_t* __restrict__ h_aff) {
-  const uint32_t m = R * K, j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  const uint32_t r = j / K, g = j % K;
+// Check records of a batched RLC check: term j (M terms, grouped by range)
+// pairs (Q_j, pk_{group[j]}) and, for the first term of each range, also
+// (S_{range[j]}, -G2).  pk_usable[g] = 0 for keys that are the identity
+// (their pairing term is 1).  S: SoA stride NR (the number of ranges);
+// Qs: stride M.  Output in k_miller's SoA input format
+// (stride M); k_miller reads the key rows through cidx = group.
+__global__ void k_rlc_pairs_list(uint32_t M, uint32_t NR, const uint32_t* __restrict__ range, const uint32_t* __restrict__ group,
+                                 const uint32_t* __restrict__ S, const uint8_t* __restrict__ pk_usable,
+                                 uint8_t* __restrict__ code, uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff,
+                                 uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ Qs) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  const uint32_t r = range[j];
   uint8_t f = 0;
   g1a s = {fp_zero(), fp_one(), true};
-  if (g == 0) s = proj_to_affine(ld_g1p(S, R, r));
+  if (j == 0 || range[j - 1] != r) s = proj_to_affine(ld_g1p(S, NR, r));
   if (s.inf) f |= INF_SIG;
-  g1a h = proj_to_affine(ld_g1p(Qs, m, j));
-  if (h.inf || !pk_usable[g]) f |= INF_PK;
-  st_fp(sig_aff, m, j, s.x);
-  st_fp(sig_aff + 12 * m, m, j, s.y);
-  st_fp(h_aff, m, j, h.x);
-  st_fp(h_aff + 12 * m, m, j, h.y);
+  g1a h = proj_to_affine(ld_g1p(Qs, M, j));
+  if (h.inf || !pk_usable[group[j]]) f |= INF_PK;
+  st_fp(sig_aff, M, j, s.x);
+  st_fp(sig_aff + 12 * M, M, j, s.y);
+  st_fp(h_aff, M, j, h.x);
+  st_fp(h_aff + 12 * M, M, j, h.y);
   inf[j] = f;
   code[j] = 0;
 }
 
-// dst (stride R*K) record j <- src (stride K) record j % K, for every uint4 row
-__global__ void k_rep_rows(uint32_t rows, uint32_t R, uint32_t K, const uint4* __restrict__ src,
-                           uint4* __restrict__ dst) {
-  const uint64_t m = (uint64_t)R * K, w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= m * rows) return;
-  const uint64_t row = w / m, j = w % m;
-  dst[row * m + j] = src[row * K + j % K];
-}
-
-// acc slot r (stride R) = prod_{g < K} fin[r*K + g] (fin stride R*K); one lane per range
-__global__ void k_fp12_prod_multi(uint32_t R, uint32_t K, const uint4* __restrict__ fin, uint4* __restrict__ acc) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const uint64_t m = (uint64_t)R * K;
-  GlobF12 a{acc, R, r};
-  copy12(a, GlobF12{const_cast<uint4*>(fin), m, r * K});
+// acc slot r (stride NR) = prod of the Miller values fin[tbeg[r] .. tbeg[r+1])
+// (fin stride M).  One 64-lane block per range: lane t multiplies every 64th
+// value into its own slot of `part` (stride NR * 64), then a tree over the
+// block; a range without terms gets one.  So a range with many key groups costs
+// ceil(cnt / 64) + 6 serial Fp12 products, not cnt.
+__global__ __launch_bounds__(64) void k_fp12_prod_segs(uint32_t NR, const uint32_t* __restrict__ tbeg,
+                                                        const uint4* __restrict__ fin, uint64_t M,
+                                                        uint4* __restrict__ part, uint4* __restrict__ acc) {
+  const uint32_t r = blockIdx.x, t = threadIdx.x;
+  if (r >= NR) return;
+  const uint64_t ps = (uint64_t)NR * 64;
+  const uint32_t b = tbeg[r], e = tbeg[r + 1];
+  GlobF12 mine{part, ps, r * 64 + t};
+  if (b + t < e) {
+    copy12(mine, GlobF12{const_cast<uint4*>(fin), M, b + t});
 #pragma unroll 1
-  for (uint32_t g = 1; g < K; g++) mul12(a, GlobF12{const_cast<uint4*>(fin), m, r * K + g});
-}
-
-// Records j < m of the K+1-pair check: pair 0 carries S (record 0 only),
-// pair 1 carries (Q_j, pk_j).  pk_usable[j] = 0 for keys that are the identity
-// (their pairing term is 1).  Output in k_miller's SoA input format (stride m).
-__global__ void k_rlc_pairs(uint32_t m, const uint32_t* __restrict__ S, const uint32_t* __restrict__ Qs,
-                            uint64_t q_stride, const uint8_t* __restrict__ pk_usable, uint8_t* __restrict__ code,
-                            uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff, uint32_t* __restrict__ h_aff) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  uint8_t f = 0;
-  g1a s = {fp_zero(), fp_one(), true};
-  if (j == 0) s = proj_to_affine(ld_g1p(S, 1, 0));
-  if (s.inf) f |= INF_SIG;
-  g1a h = proj_to_affine(ld_g1p(Qs, q_stride, j));
-  if (h.inf || !pk_usable[j]) f |= INF_PK;
-  st_fp(sig_aff, m, j, s.x);
-  st_fp(sig_aff + 12 * m, m, j, s.y);
-  st_fp(h_aff, m, j, h.x);
-  st_fp(h_aff + 12 * m, m, j, h.y);
-  inf[j] = f;
-  code[j] = 0;
-}
-
-// acc (stride-1 slot) = prod_{j < m} fin[j]  (fin: uint4 SoA with stride fstride)
-__global__ void k_fp12_prod(uint32_t m, const uint4* __restrict__ fin, uint64_t fstride, uint4* __restrict__ acc) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  GlobF12 a{acc, 1, 0};
-  copy12(a, GlobF12{const_cast<uint4*>(fin), fstride, 0});
+    for (uint32_t j = b + t + 64; j < e; j += 64) mul12(mine, GlobF12{const_cast<uint4*>(fin), M, j});
+  } else {
+    set_one12(mine);
+  }
 #pragma unroll 1
-  for (uint32_t j = 1; j < m; j++) mul12(a, GlobF12{const_cast<uint4*>(fin), fstride, j});
+  for (uint32_t s = 32; s >= 1; s >>= 1) {
+    __syncthreads();
+    if (t < s) mul12(mine, GlobF12{part, ps, r * 64 + t + s});
+  }
+  __syncthreads();
+  if (t == 0) copy12(GlobF12{acc, NR, r}, mine);
 }
 
 // code[0] = 0 iff prod_{j < m} gt_j == 1; gts: m canonical Gt values (576 B,

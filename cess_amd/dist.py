@@ -1,10 +1,17 @@
-"""Multi-GPU sharding of a verification batch (one process per GPU).
+"""Multi-GPU sharding of a verification batch (one process per GPU) for
+callers that already run a torch.distributed process group.
+
+The product path does NOT need this module: the C-ABI library owns an RCCL
+communicator (cess_bls_comm_init) and all-gathers verdict bitmaps, codes and
+RLC Gt partials itself (cess_bls_verify_batch_sharded*, _rlc_sharded), which is
+what bench.py and C/Rust callers use.  This module restates the same shard
+layout (cess_bls_shard_range) and protocol over torch.distributed (gloo on CPU
+in the tests, RCCL/"nccl" on GPUs).
 
 Signatures are independent (reference src/lib.rs:243 is per signature), so a
 batch shards by index with no exchange during compute.  The only collective is
-the all-gather of the per-rank verdict-bitmap words (RCCL over xGMI on the
-node; gloo in CPU tests), which gives every rank the full batch bitmap — what a
-node-side caller of verify_batch needs.
+the all-gather of the per-rank verdict-bitmap words, which gives every rank the
+full batch bitmap -- what a node-side caller of verify_batch needs.
 """
 from __future__ import annotations
 
@@ -12,16 +19,16 @@ from typing import Tuple
 
 
 def shard_range(n: int, rank: int, world: int, align: int = 64) -> Tuple[int, int]:
-    """Contiguous [start, end) of rank's shard; boundaries are multiples of
-    `align` (a whole number of bitmap words per rank) except the batch end."""
+    """Contiguous [start, end) of rank's shard, the layout of the library's
+    cess_bls_shard_range: ceil(n / 64) bitmap words split into `world` equal
+    runs of ceil(words / world) words (the last shards may be short or empty),
+    so every shard is whole bitmap words and an all-gather of equal-size blocks
+    concatenates to the batch bitmap with no re-packing."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError("bad rank/world")
     words = (n + align - 1) // align
-    per = words // world
-    extra = words % world
-    w0 = rank * per + min(rank, extra)
-    w1 = w0 + per + (1 if rank < extra else 0)
-    return min(n, w0 * align), min(n, w1 * align)
+    per = (words + world - 1) // world
+    return min(n, rank * per * align), min(n, (rank + 1) * per * align)
 
 
 def gather_bitmap(local_words, n: int, world: int, group=None):
@@ -33,11 +40,8 @@ def gather_bitmap(local_words, n: int, world: int, group=None):
 
     if world == 1:
         return local_words
-    sizes = []
-    for r in range(world):
-        a, b = shard_range(n, r, world)
-        sizes.append((b - a + 63) // 64)
-    mx = max(sizes)
+    words = (n + 63) // 64
+    mx = (words + world - 1) // world
     buf = torch.zeros(mx, dtype=torch.int64, device=local_words.device)
     buf[: local_words.numel()] = local_words
     out = torch.empty(world * mx, dtype=torch.int64, device=local_words.device)
@@ -47,7 +51,7 @@ def gather_bitmap(local_words, n: int, world: int, group=None):
         out = torch.cat(parts)
     else:
         dist.all_gather_into_tensor(out, buf, group=group)
-    return torch.cat([out[r * mx: r * mx + sizes[r]] for r in range(world)])
+    return out[:words]
 
 
 def shard_seed(seed: bytes, rank: int) -> bytes:
@@ -62,9 +66,11 @@ def verify_rlc_sharded(ctx, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets, s
                        rank: int, world: int, device=None, group=None):
     """RLC batch mode across ranks: every rank checks its shard
     and contributes its Gt partial; the partials are all-gathered (RCCL over
-    xGMI; gloo on CPU) and multiplied on the device; only a rank whose own
-    partial fails bisects.  Arguments are this rank's shard (fixed-stride
-    records); returns (codes, bitmap words, stats) for the shard."""
+    xGMI; gloo on CPU) and multiplied on the device for the batch-level
+    verdict; a rank bisects iff its OWN check failed (rlc_finish), so no other
+    rank's partial can cancel a local failure.  Arguments are this rank's shard
+    (fixed-stride records); returns (codes, bitmap words, stats) for the shard.
+    `seed` must be secret and unpredictable to the signers (include/cess_bls.h)."""
     import torch
     import torch.distributed as dist
 

@@ -6,6 +6,11 @@
  * names the reference interface it replaces.  Plain pointers and sizes only; the
  * caller owns every buffer.  A context is used by one host thread at a time.
  *
+ * Concurrency: a context is used by one host thread at a time; a call that
+ * finds another thread inside the same context returns CESS_BLS_E_BUSY.
+ * Successive calls on one context are ordered on the device even when they
+ * name different streams (each call waits for the previous call's work).
+ *
  * Return values of every function are INFRASTRUCTURE status (CESS_BLS_OK or a
  * negative CESS_BLS_E_* code).  Verification verdicts are returned separately as
  * per-signature codes:
@@ -37,6 +42,10 @@ extern "C" {
 #define CESS_BLS_E_HIP (-3)
 #define CESS_BLS_E_OOM (-4)
 #define CESS_BLS_E_RCCL (-5)
+#define CESS_BLS_E_BUSY (-6)     /* another host thread is inside a call on this context */
+#define CESS_BLS_E_BAD_KEY (-7)  /* cess_bls_enclave_verify_bls: the key does not deserialize (the reference panics) */
+#define CESS_BLS_E_BAD_SIG (-8)  /* cess_bls_enclave_verify_bls: the signature does not deserialize (the reference panics) */
+#define CESS_BLS_E_NO_COMM (-9)  /* a sharded entry point on a context without cess_bls_comm_init */
 
 enum cess_bls_code {
   CESS_BLS_CODE_OK = 0,
@@ -51,16 +60,33 @@ enum cess_bls_code {
 #define CESS_BLS_PK_BYTES 96   /* PublicKey::BYTES  src/lib.rs:56  */
 #define CESS_BLS_SK_BYTES 32   /* PrivateKey::BYTES src/lib.rs:178 */
 #define CESS_BLS_GT_BYTES 576
+#define CESS_BLS_COMM_ID_BYTES 128  /* ncclUniqueId */
 
 typedef struct cess_bls_ctx cess_bls_ctx;
 
+/* Context configuration (SURVEY §8(b) bls_ctx_create: device set, batch size,
+ * mode, strict-identity flag).  Zero-initialise and set what you need. */
 typedef struct cess_bls_config {
-  int device;          /* HIP device ordinal (-1: current device)                  */
-  uint64_t max_batch;  /* signatures per device launch chunk (0: default 1<<20)    */
-  uint32_t flags;      /* CESS_BLS_F_* */
+  int device;          /* HIP device ordinal of a single-device context (-1: device 0)           */
+  uint64_t max_batch;  /* signatures per device launch chunk (0: default 1<<20)                  */
+  uint32_t flags;      /* CESS_BLS_F_*                                                            */
+  uint32_t mode;       /* CESS_BLS_MODE_*: what cess_bls_verify_batch runs                       */
+  int n_devices;       /* > 1: one context over several GPUs of this process: host-buffer batches
+                          are sharded by index across them (one host thread per device)          */
+  const int* devices;  /* n_devices ordinals (NULL: 0 .. n_devices-1); may repeat an ordinal      */
 } cess_bls_config;
 
-#define CESS_BLS_F_PROFILE 1u /* record per-stage HIP event timings */
+#define CESS_BLS_F_PROFILE 1u          /* record per-stage HIP event timings */
+/* Reject identity public keys (0xc0 || 0^95) with CESS_BLS_CODE_PK_POINT, as the
+ * IETF KeyValidate does.  Off by default: the reference accepts them
+ * (PublicKey::deserialize, src/lib.rs:68-82, has no identity check), so the
+ * (sig = O, pk = O) pair verifies for every message. */
+#define CESS_BLS_F_STRICT_IDENTITY 2u
+
+#define CESS_BLS_MODE_PER_SIG 0u  /* two-pairing check per signature (default; src/lib.rs:85-100)      */
+/* random linear combination with bisection (cess_bls_verify_batch_rlc semantics):
+ * cess_bls_verify_batch draws a fresh 32-byte seed from the OS CSPRNG per call */
+#define CESS_BLS_MODE_RLC 1u
 
 /* Context: device buffers, stream, and the G2PREPARED_NEG_G table
  * (replaces the lazy_static at src/lib.rs:19-21). */
@@ -111,8 +137,9 @@ int cess_bls_verify_batch_keyed(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs
                                 const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* codes_out,
                                 uint64_t* bitmap_out);
 
-/* Device-resident keyed batch (as cess_bls_verify_batch_device; the caller
- * guarantees every d_key_idx[i] < k). */
+/* Device-resident keyed batch (as cess_bls_verify_batch_device).  A record whose
+ * d_key_idx[i] >= k is rejected on the device with CESS_BLS_CODE_PK_POINT (its
+ * key does not exist), so no out-of-range table row is ever read. */
 int cess_bls_verify_batch_keyed_device(cess_bls_ctx* ctx, size_t n, const uint8_t* d_sigs,
                                        const uint32_t* d_key_idx, const uint8_t* d_msgs,
                                        const uint64_t* d_msg_offsets, uint8_t* d_codes, uint64_t* d_bitmap,
@@ -141,25 +168,103 @@ int cess_bls_gt_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const ui
  * mode"; no reference counterpart).  For records with distinct keys
  * pk_1..pk_K, one check
  *     e(sum r_i sig_i, -G2) * prod_k e(sum_{pk_i = pk_k} r_i H(m_i), pk_k) == 1
- * (r_i: 128-bit, derived from `seed32` by SHA-256) replaces n pairing
+ * (r_i: 128-bit, r_i = SHA-256(seed32 || index)[0:16] | 1) replaces n pairing
  * products; a failing batch is bisected down to leaves verified per signature,
  * so codes_out equals cess_bls_verify_batch's except with probability 2^-127
- * per check.  Fixed-stride records (48-B sigs, 96-B keys), host buffers. */
+ * per check.  Fixed-stride records (48-B sigs, 96-B keys), host buffers.
+ *
+ * SECURITY: seed32 MUST be secret and unpredictable to whoever produced the
+ * signatures (fresh CSPRNG output per call, never reused, never derived from
+ * the batch).  With a seed the signer can predict, forgeries can be crafted
+ * whose errors cancel in the combination and the batch reports them valid.
+ * Pass seed32 = NULL to have the library draw one from the OS CSPRNG
+ * (getrandom(2)).  Batches with more than one distinct key per 8 records gain
+ * nothing from a combination and are verified per signature. */
 int cess_bls_verify_batch_rlc(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks,
                               const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
                               uint8_t* codes_out, uint64_t* bitmap_out,
                               uint64_t* stats4 /* checks, leaves, leaf sigs, distinct keys; may be NULL */);
 
-/* Multi-GPU form (one shard per context): rlc_begin runs the shard's check and
- * returns its Gt partial (576 canonical bytes); the caller all-gathers the
- * partials (RCCL), combines them with cess_bls_gt_product_is_one, and passes
- * the global verdict to rlc_finish, which bisects the shard if needed.  The
- * record buffers must stay valid until rlc_finish returns. */
+/* Multi-GPU form driven by the caller's own collectives (one shard per
+ * context): rlc_begin runs the shard's check and returns its Gt partial (576
+ * canonical bytes); the caller all-gathers the partials, combines them with
+ * cess_bls_gt_product_is_one (a batch-level verdict), and calls rlc_finish,
+ * which bisects the shard whenever the shard's OWN check failed -- whatever
+ * the combined verdict, so other shards' partials can never cancel a local
+ * failure.  global_ok is accepted for the record only.  The record buffers
+ * must stay valid until rlc_finish returns.  seed32 as above (NULL: OS CSPRNG). */
 int cess_bls_rlc_begin(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
                        const uint64_t* msg_offsets, const uint8_t* seed32, uint8_t* gt_out);
 int cess_bls_gt_product_is_one(cess_bls_ctx* ctx, size_t m, const uint8_t* gts, int* is_one);
 int cess_bls_rlc_finish(cess_bls_ctx* ctx, int global_ok, uint8_t* codes_out, uint64_t* bitmap_out,
                         uint64_t* stats4);
+
+/* ---- multi-GPU: RCCL communicator in the context ----
+ * One process and one context per GPU.  Signatures are independent
+ * (src/lib.rs:243 is per signature), so a batch shards by index with no
+ * exchange during compute; the only collectives are RCCL all-gathers (over
+ * xGMI on one node) of the verdict-bitmap words, optionally of the code bytes,
+ * and in RLC mode of the 576-byte Gt partials. */
+
+/* ncclGetUniqueId on one rank (e.g. rank 0); the caller distributes the 128
+ * bytes to every rank out of band. */
+int cess_bls_comm_id(uint8_t id_out[CESS_BLS_COMM_ID_BYTES]);
+/* ncclCommInitRank on the context's device (collective: every rank calls it). */
+int cess_bls_comm_init(cess_bls_ctx* ctx, int nranks, int rank, const uint8_t id[CESS_BLS_COMM_ID_BYTES]);
+/* Records [*begin, *end) of rank's shard of an n-record batch: ceil(n/64)
+ * bitmap words split into nranks equal runs of *words_per_rank words (the last
+ * shards may be short or empty), so shards are whole bitmap words and the
+ * all-gather needs no re-packing.  Pure function (no context). */
+int cess_bls_shard_range(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end,
+                         uint64_t* words_per_rank);
+/* Sharded host-buffer batch (collective): every rank passes the WHOLE batch;
+ * rank r verifies its shard, then codes and bitmap words are all-gathered, so
+ * every rank returns the verdicts of all n records.  codes_out (n bytes) and
+ * bitmap_out (ceil(n/64) words) may be NULL. */
+int cess_bls_verify_batch_sharded(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks,
+                                  const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* codes_out,
+                                  uint64_t* bitmap_out);
+/* Device-resident sharded batch (collective): d_sigs/d_pks/d_msgs/d_msg_offsets
+ * hold only this rank's shard (cess_bls_shard_range; offsets shard-local,
+ * shard_n + 1 entries).  d_bitmap_all (nranks * words_per_rank words) receives
+ * the full batch bitmap; d_codes_all (nranks * words_per_rank * 64 bytes, may
+ * be NULL) the full code array (bytes past n unspecified).  Enqueued on
+ * `stream` (NULL: the context's), not synchronised. */
+int cess_bls_verify_batch_sharded_device(cess_bls_ctx* ctx, size_t n_total, const uint8_t* d_sigs,
+                                         const uint8_t* d_pks, const uint8_t* d_msgs,
+                                         const uint64_t* d_msg_offsets, uint8_t* d_codes_all,
+                                         uint64_t* d_bitmap_all, void* stream);
+/* RLC over the communicator (collective): each rank passes its own shard
+ * (n_shard fixed-stride records), checks it with one combination (scalars
+ * distinct across ranks), the Gt partials are all-gathered over RCCL and
+ * multiplied on the device (*global_ok_out: the whole batch passed, may be
+ * NULL), and a rank bisects iff its own check failed.  Codes/bitmap cover
+ * the shard.  seed32 as cess_bls_verify_batch_rlc (every rank may pass its
+ * own; NULL: OS CSPRNG). */
+int cess_bls_verify_batch_rlc_sharded(cess_bls_ctx* ctx, size_t n_shard, const uint8_t* sigs, const uint8_t* pks,
+                                      const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
+                                      uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4,
+                                      int* global_ok_out);
+/* Control-plane helpers over the same communicator (collective). */
+int cess_bls_comm_barrier(cess_bls_ctx* ctx);
+int cess_bls_comm_max_f64(cess_bls_ctx* ctx, double* value);
+
+/* ---- device memory on the context's GPU (for callers without a HIP runtime
+ * of their own: keep a batch resident in HBM across device-resident calls) */
+int cess_bls_device_alloc(cess_bls_ctx* ctx, size_t bytes, void** d_out);
+int cess_bls_device_free(cess_bls_ctx* ctx, void* d);
+int cess_bls_copy_to_device(cess_bls_ctx* ctx, void* d_dst, const void* src, size_t bytes);
+int cess_bls_copy_from_device(cess_bls_ctx* ctx, void* dst, const void* d_src, size_t bytes);
+int cess_bls_synchronize(cess_bls_ctx* ctx);
+
+/* cp_enclave_verify::verify_bls(key, msg, sig) (primitives/enclave-verify/src/
+ * lib.rs:230-235): NOTE the reversed argument order.  The key is decoded first
+ * (PublicKey::deserialize(key).unwrap(), :231), then the signature (:233);
+ * where the reference panics this returns CESS_BLS_E_BAD_KEY / _BAD_SIG
+ * instead.  Otherwise CESS_BLS_OK with *ok_out = 1 iff puk.verify(msg, sig)
+ * is Ok(()). */
+int cess_bls_enclave_verify_bls(cess_bls_ctx* ctx, const uint8_t* key, size_t key_len, const uint8_t* msg,
+                                size_t msg_len, const uint8_t* sig, size_t sig_len, int* ok_out);
 
 /* Per-stage timings (ms, summed since the last reset) when CESS_BLS_F_PROFILE is
  * set.  names/ms arrays of length max; returns the number of stages. */

@@ -62,7 +62,7 @@ def test_gather_matches_single(n, world):
 
 
 def test_shard_ranges_cover_and_align():
-    for n in (1, 63, 64, 65, 1 << 20, 16 * (1 << 20) + 5):
+    for n in (0, 1, 63, 64, 65, 1 << 20, 16 * (1 << 20) + 5):
         for world in (1, 2, 3, 8):
             prev = 0
             for r in range(world):
@@ -72,6 +72,20 @@ def test_shard_ranges_cover_and_align():
             assert prev == n
 
 
+def test_shard_ranges_match_library():
+    """dist.shard_range restates the C ABI's cess_bls_shard_range (a pure
+    function: callable without a GPU); bench.py's config[2] shards are exact."""
+    from cess_amd import bls
+    for n in (0, 1, 63, 64, 65, 4096, 1 << 20, 16 * (1 << 20) + 5, 16 << 20):
+        for world in (1, 2, 3, 4, 8):
+            wpr = ((n + 63) // 64 + world - 1) // world
+            for r in range(world):
+                assert bls.shard_range(n, world, r) == shard_range(n, r, world) + (wpr,)
+    for world in (2, 4, 8):   # config[2]: 2 M per GPU
+        for r in range(world):
+            assert bls.shard_range(world << 21, world, r)[:2] == (r << 21, (r + 1) << 21)
+
+
 # --- RLC orchestration (cess_amd.dist.verify_rlc_sharded) ------------------
 GT_ONE = bytes(47) + b"\x01" + bytes(528)
 
@@ -79,7 +93,9 @@ GT_ONE = bytes(47) + b"\x01" + bytes(528)
 class _ShardCtx:
     """Stand-in for a GPU context: a record is 'valid' iff its message byte 0
     is even.  The Gt partial is one iff the shard is all valid (the algebra is
-    the GPU's; this checks the cross-rank protocol)."""
+    the GPU's; this checks the cross-rank protocol).  rlc_finish follows the
+    library: a shard bisects iff its own check failed, whatever the combined
+    verdict (bisection then yields exact codes)."""
 
     def rlc_begin(self, sigs, pks, msgs, offs, seed):
         self.seed = seed
@@ -90,7 +106,8 @@ class _ShardCtx:
         return all(gts[i:i + 576] == GT_ONE for i in range(0, len(gts), 576))
 
     def rlc_finish(self, ok):
-        codes = bytes(0 if (ok or v) else 5 for v in self.valid)
+        local_ok = all(self.valid)
+        codes = bytes(0 if (local_ok or v) else 5 for v in self.valid)
         return codes, [], {"checks": 1}
 
 

@@ -80,6 +80,11 @@ def test_verify_batch_dedups_keys(ctx, vectors):
     recs = [(bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])) for c in cases]
     recs = (recs * (1 + 2048 // max(len(recs), 1)))[:2048]
     assert 8 * len({r[2] for r in recs}) <= len(recs)
-    v = bls.verify_batch(recs, ctx=ctx)
+    c = bls.Context(max_batch=4096)      # no caller-loaded key table: the dedup path runs
+    try:
+        v = bls.verify_batch(recs, ctx=c)
+        assert c._keys_owner == "verify_batch"
+    finally:
+        c.close()
     ref = bls.verify_batch(recs, ctx=ctx, dedup_keys=False)
     assert v.codes == ref.codes and v.bitmap == ref.bitmap

@@ -197,11 +197,12 @@ def test_rlc_local_failure_bisects_despite_global_ok(ctx):
     assert codes[999] == 5 and codes.count(0) == 2499
 
 
-@pytest.mark.parametrize("nkeys,forged", [(1000, [3, 1500, 3999]), (256, [10, 2000])])
+@pytest.mark.parametrize("nkeys,forged", [(1000, [3, 1500, 3999]), (1024, [10, 9000])])
 def test_rlc_many_keys(ctx, nkeys, forged):
     """K > n/8: per-signature fallback; K = n/16: bisection over term lists
-    (no NR x K replication)."""
-    n = 4000 if nkeys == 1000 else 4096
+    (no NR x K replication): 16,384 records split into 8 ranges of 2,048, of
+    which at most the two holding a forgery are verified per signature."""
+    n = 4000 if nkeys == 1000 else 16384
     sigs, msgs, pks = _signed(ctx, n, 42 + nkeys, keys=nkeys)
     for i in forged:
         msgs[i] = bytes(32)

@@ -1,0 +1,122 @@
+//! Raw bindings of include/cess_bls.h (one `extern "C"` item per header entry
+//! point; the comments name the reference interface each one replaces).
+//! NOT COMPILED in this repository's image (no cargo).
+#![allow(non_camel_case_types)]
+
+use core::ffi::{c_char, c_int, c_void};
+
+pub const CESS_BLS_OK: c_int = 0;
+pub const CESS_BLS_E_INVALID_ARG: c_int = -1;
+pub const CESS_BLS_E_NO_DEVICE: c_int = -2;
+pub const CESS_BLS_E_HIP: c_int = -3;
+pub const CESS_BLS_E_OOM: c_int = -4;
+pub const CESS_BLS_E_RCCL: c_int = -5;
+pub const CESS_BLS_E_BUSY: c_int = -6;
+pub const CESS_BLS_E_BAD_KEY: c_int = -7;
+pub const CESS_BLS_E_BAD_SIG: c_int = -8;
+pub const CESS_BLS_E_NO_COMM: c_int = -9;
+
+pub const CODE_OK: u8 = 0;
+pub const CODE_SIG_LEN: u8 = 1;
+pub const CODE_SIG_POINT: u8 = 2;
+pub const CODE_PK_LEN: u8 = 3;
+pub const CODE_PK_POINT: u8 = 4;
+pub const CODE_PAIRING_FAIL: u8 = 5;
+
+pub const CESS_BLS_F_PROFILE: u32 = 1;
+pub const CESS_BLS_F_STRICT_IDENTITY: u32 = 2;
+pub const CESS_BLS_MODE_PER_SIG: u32 = 0;
+pub const CESS_BLS_MODE_RLC: u32 = 1;
+pub const CESS_BLS_COMM_ID_BYTES: usize = 128;
+
+#[repr(C)]
+pub struct cess_bls_config {
+    pub device: c_int,
+    pub max_batch: u64,
+    pub flags: u32,
+    pub mode: u32,
+    pub n_devices: c_int,
+    pub devices: *const c_int,
+}
+
+#[repr(C)]
+pub struct cess_bls_ctx {
+    _private: [u8; 0],
+}
+
+extern "C" {
+    // context (G2PREPARED_NEG_G, utils/verify-bls-signatures/src/lib.rs:19-21, plus device state)
+    pub fn cess_bls_ctx_create(cfg: *const cess_bls_config, out: *mut *mut cess_bls_ctx) -> c_int;
+    pub fn cess_bls_ctx_destroy(ctx: *mut cess_bls_ctx);
+    // verify_bls_signature (src/lib.rs:243-247)
+    pub fn cess_bls_verify(ctx: *mut cess_bls_ctx, sig: *const u8, sig_len: usize, msg: *const u8, msg_len: usize,
+                           key: *const u8, key_len: usize, code_out: *mut u8) -> c_int;
+    // verify_batch (new)
+    pub fn cess_bls_verify_batch(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8, msgs: *const u8,
+                                 msg_offsets: *const u64, codes_out: *mut u8, bitmap_out: *mut u64) -> c_int;
+    pub fn cess_bls_verify_batch_var(ctx: *mut cess_bls_ctx, n: usize, sig_data: *const u8, sig_offsets: *const u64,
+                                     pk_data: *const u8, pk_offsets: *const u64, msgs: *const u8,
+                                     msg_offsets: *const u64, codes_out: *mut u8, bitmap_out: *mut u64) -> c_int;
+    pub fn cess_bls_verify_batch_device(ctx: *mut cess_bls_ctx, n: usize, d_sigs: *const u8, d_pks: *const u8,
+                                        d_msgs: *const u8, d_msg_offsets: *const u64, d_codes: *mut u8,
+                                        d_bitmap: *mut u64, stream: *mut c_void) -> c_int;
+    // distinct-key table (PublicKey::deserialize :68-82 + G2Prepared::from :88 once per key)
+    pub fn cess_bls_keys_load(ctx: *mut cess_bls_ctx, k: usize, pks: *const u8, key_codes_out: *mut u8) -> c_int;
+    pub fn cess_bls_verify_batch_keyed(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, key_idx: *const u32,
+                                       msgs: *const u8, msg_offsets: *const u64, codes_out: *mut u8,
+                                       bitmap_out: *mut u64) -> c_int;
+    pub fn cess_bls_verify_batch_keyed_device(ctx: *mut cess_bls_ctx, n: usize, d_sigs: *const u8,
+                                              d_key_idx: *const u32, d_msgs: *const u8, d_msg_offsets: *const u64,
+                                              d_codes: *mut u8, d_bitmap: *mut u64, stream: *mut c_void) -> c_int;
+    // PrivateKey::public_key (:226-228), PrivateKey::sign (:233-236), hash_to_g1 (:25-31)
+    pub fn cess_bls_public_key_batch(ctx: *mut cess_bls_ctx, n: usize, sks: *const u8, pks_out: *mut u8) -> c_int;
+    pub fn cess_bls_sign_batch(ctx: *mut cess_bls_ctx, n: usize, sks: *const u8, msgs: *const u8,
+                               msg_offsets: *const u64, sigs_out: *mut u8) -> c_int;
+    pub fn cess_bls_hash_to_g1_batch(ctx: *mut cess_bls_ctx, n: usize, msgs: *const u8, msg_offsets: *const u64,
+                                     out48: *mut u8) -> c_int;
+    pub fn cess_bls_gt_batch(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8, msgs: *const u8,
+                             msg_offsets: *const u64, codes_out: *mut u8, gt_out: *mut u8) -> c_int;
+    // RLC batch mode (north_star); seed32 NULL = library CSPRNG
+    pub fn cess_bls_verify_batch_rlc(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8,
+                                     msgs: *const u8, msg_offsets: *const u64, seed32: *const u8,
+                                     codes_out: *mut u8, bitmap_out: *mut u64, stats4: *mut u64) -> c_int;
+    pub fn cess_bls_rlc_begin(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8, msgs: *const u8,
+                              msg_offsets: *const u64, seed32: *const u8, gt_out: *mut u8) -> c_int;
+    pub fn cess_bls_gt_product_is_one(ctx: *mut cess_bls_ctx, m: usize, gts: *const u8, is_one: *mut c_int) -> c_int;
+    pub fn cess_bls_rlc_finish(ctx: *mut cess_bls_ctx, global_ok: c_int, codes_out: *mut u8, bitmap_out: *mut u64,
+                               stats4: *mut u64) -> c_int;
+    // multi-GPU: RCCL communicator in the context
+    pub fn cess_bls_comm_id(id_out: *mut u8) -> c_int;
+    pub fn cess_bls_comm_init(ctx: *mut cess_bls_ctx, nranks: c_int, rank: c_int, id: *const u8) -> c_int;
+    pub fn cess_bls_shard_range(n: u64, nranks: c_int, rank: c_int, begin: *mut u64, end: *mut u64,
+                                words_per_rank: *mut u64) -> c_int;
+    pub fn cess_bls_verify_batch_sharded(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8,
+                                         msgs: *const u8, msg_offsets: *const u64, codes_out: *mut u8,
+                                         bitmap_out: *mut u64) -> c_int;
+    pub fn cess_bls_verify_batch_sharded_device(ctx: *mut cess_bls_ctx, n_total: usize, d_sigs: *const u8,
+                                                d_pks: *const u8, d_msgs: *const u8, d_msg_offsets: *const u64,
+                                                d_codes_all: *mut u8, d_bitmap_all: *mut u64,
+                                                stream: *mut c_void) -> c_int;
+    pub fn cess_bls_verify_batch_rlc_sharded(ctx: *mut cess_bls_ctx, n_shard: usize, sigs: *const u8,
+                                             pks: *const u8, msgs: *const u8, msg_offsets: *const u64,
+                                             seed32: *const u8, codes_out: *mut u8, bitmap_out: *mut u64,
+                                             stats4: *mut u64, global_ok_out: *mut c_int) -> c_int;
+    pub fn cess_bls_comm_barrier(ctx: *mut cess_bls_ctx) -> c_int;
+    pub fn cess_bls_comm_max_f64(ctx: *mut cess_bls_ctx, value: *mut f64) -> c_int;
+    // device memory on the context's GPU
+    pub fn cess_bls_device_alloc(ctx: *mut cess_bls_ctx, bytes: usize, d_out: *mut *mut c_void) -> c_int;
+    pub fn cess_bls_device_free(ctx: *mut cess_bls_ctx, d: *mut c_void) -> c_int;
+    pub fn cess_bls_copy_to_device(ctx: *mut cess_bls_ctx, d_dst: *mut c_void, src: *const c_void,
+                                   bytes: usize) -> c_int;
+    pub fn cess_bls_copy_from_device(ctx: *mut cess_bls_ctx, dst: *mut c_void, d_src: *const c_void,
+                                     bytes: usize) -> c_int;
+    pub fn cess_bls_synchronize(ctx: *mut cess_bls_ctx) -> c_int;
+    // cp_enclave_verify::verify_bls (primitives/enclave-verify/src/lib.rs:230-235)
+    pub fn cess_bls_enclave_verify_bls(ctx: *mut cess_bls_ctx, key: *const u8, key_len: usize, msg: *const u8,
+                                       msg_len: usize, sig: *const u8, sig_len: usize, ok_out: *mut c_int) -> c_int;
+    // diagnostics
+    pub fn cess_bls_stage_times(ctx: *mut cess_bls_ctx, names: *mut *const c_char, ms: *mut f64, max: c_int,
+                                reset: c_int) -> c_int;
+    pub fn cess_bls_status_string(status: c_int) -> *const c_char;
+    pub fn cess_bls_version() -> *const c_char;
+}

@@ -44,7 +44,14 @@ EXPORTS = (
     "cess_bls_verify_batch_sharded_device", "cess_bls_verify_batch_rlc_sharded", "cess_bls_comm_barrier",
     "cess_bls_comm_max_f64", "cess_bls_device_alloc", "cess_bls_device_free", "cess_bls_copy_to_device",
     "cess_bls_copy_from_device", "cess_bls_synchronize", "cess_bls_enclave_verify_bls",
+    "cess_bls_stage_stats", "cess_bls_launch_records",
+    # include/cess_rsa.h (RSA PKCS#1 v1.5 raw verify, cp_enclave_verify::verify_rsa)
+    "cess_rsa_parse_key", "cess_rsa_keys_load", "cess_rsa_verify_batch", "cess_rsa_verify_batch_device",
+    "cess_rsa_verify",
 )
+RSA_E_UNSUPPORTED = -10
+RSA_KEY_SPKI, RSA_KEY_PKCS1 = 0, 1
+RSA_CODE_NAMES = {0: "OK", 1: "SIG_LEN", 2: "SIG_RANGE", 3: "MSG_LEN", 4: "MISMATCH", 5: "KEY"}
 
 # infrastructure status codes (include/cess_bls.h)
 E_INVALID_ARG, E_NO_DEVICE, E_HIP, E_OOM, E_RCCL, E_BUSY, E_BAD_KEY, E_BAD_SIG, E_NO_COMM = range(-1, -10, -1)
@@ -118,6 +125,16 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_copy_from_device.argtypes = [vp, vp, vp, sz]
         lib.cess_bls_synchronize.argtypes = [vp]
         lib.cess_bls_enclave_verify_bls.argtypes = [vp, _u8p, sz, _u8p, sz, _u8p, sz, ctypes.POINTER(ctypes.c_int)]
+        lib.cess_rsa_parse_key.argtypes = [_u8p, sz, ctypes.c_int, _u8p, sz, ctypes.POINTER(ctypes.c_size_t), _u64p]
+        lib.cess_rsa_keys_load.argtypes = [vp, sz, _u8p, _u64p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        lib.cess_rsa_verify_batch.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), _u8p, _u64p, _u8p, _u64p, _u8p,
+                                              _u64p]
+        lib.cess_rsa_verify_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
+        lib.cess_rsa_verify.argtypes = [vp, _u8p, sz, _u8p, sz, _u8p, sz, ctypes.POINTER(ctypes.c_int)]
+        lib.cess_bls_stage_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                             _u64p, ctypes.c_int, ctypes.c_int]
+        lib.cess_bls_launch_records.argtypes = [vp]
+        lib.cess_bls_launch_records.restype = ctypes.c_uint64
         lib.cess_bls_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                              ctypes.c_int, ctypes.c_int]
         lib.cess_bls_status_string.restype = ctypes.c_char_p
@@ -420,6 +437,39 @@ class Context:
                                                         len(sig), ctypes.byref(ok)))
         return bool(ok.value)
 
+    # --- RSA PKCS#1 v1.5 raw verify (include/cess_rsa.h) -------------------
+    def rsa_keys_load(self, ders: Sequence[bytes], fmt: int = RSA_KEY_SPKI) -> list:
+        """Load the RSA key table (DER keys); returns per-key status (0, E_BAD_KEY, RSA_E_UNSUPPORTED)."""
+        k = len(ders)
+        st = (ctypes.c_int * max(k, 1))()
+        self._chk(self._lib.cess_rsa_keys_load(self._h, k, _buf(b"".join(bytes(d) for d in ders)),
+                                               _offsets([len(d) for d in ders]), fmt, st))
+        return list(st)[:k]
+
+    def rsa_verify_batch(self, key_idx: Sequence[int], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> bytes:
+        """verify_rsa over records (key key_idx[i] of the loaded table): per-record codes."""
+        n = len(key_idx)
+        idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        self._chk(self._lib.cess_rsa_verify_batch(self._h, n, idx, _buf(b"".join(sigs)), _offsets([len(x) for x in sigs]),
+                                                  _buf(b"".join(msgs)), _offsets([len(m) for m in msgs]), codes,
+                                                  bitmap))
+        return bytes(codes)[:n]
+
+    def rsa_verify_batch_device(self, n, d_key_idx, d_sigs, d_sig_offs, d_msgs, d_msg_offs, d_codes, stream=0):
+        self._chk(self._lib.cess_rsa_verify_batch_device(self._h, n, d_key_idx, d_sigs, d_sig_offs, d_msgs, d_msg_offs,
+                                                         d_codes, stream or None))
+
+    def verify_rsa(self, key_der: bytes, msg: bytes, sig: bytes) -> bool:
+        """cp_enclave_verify::verify_rsa (enclave-verify/src/lib.rs:221-228); raises
+        BlsInfraError(E_BAD_KEY) where from_public_key_der(key).unwrap() panics."""
+        ok = ctypes.c_int()
+        key_der, msg, sig = bytes(key_der), bytes(msg), bytes(sig)
+        self._chk(self._lib.cess_rsa_verify(self._h, _buf(key_der), len(key_der), _buf(msg), len(msg), _buf(sig),
+                                            len(sig), ctypes.byref(ok)))
+        return bool(ok.value)
+
     # --- generator side -------------------------------------------------
     def public_keys_raw(self, sks: bytes) -> bytes:
         """n concatenated 32-byte secret keys -> n concatenated 96-byte keys."""
@@ -459,6 +509,18 @@ class Context:
         raw = bytes(out)
         return [raw[48 * i:48 * (i + 1)] for i in range(n)]
 
+    def stage_stats(self, reset=True) -> dict:
+        """{stage: (ms summed over launches, launches)} since the last reset."""
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_double * 16)()
+        ln = (ctypes.c_uint64 * 16)()
+        k = self._lib.cess_bls_stage_stats(self._h, names, ms, ln, 16, 1 if reset else 0)
+        return {names[i].decode(): (ms[i], ln[i]) for i in range(k)}
+
+    @property
+    def launch_records(self) -> int:
+        return int(self._lib.cess_bls_launch_records(self._h))
+
     def stage_times(self, reset=True) -> dict:
         names = (ctypes.c_char_p * 16)()
         ms = (ctypes.c_double * 16)()
@@ -477,6 +539,18 @@ def shard_range(n: int, nranks: int, rank: int) -> Tuple[int, int, int]:
     if st != 0:
         raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
     return b.value, e.value, w.value
+
+
+def rsa_parse_key(der: bytes, fmt: int = RSA_KEY_SPKI) -> Tuple[bytes, int]:
+    """(modulus big-endian, e) of a DER RSA public key (host-side parse)."""
+    lib = load_library()
+    der = bytes(der)
+    out = (ctypes.c_uint8 * 512)()
+    ln, e = ctypes.c_size_t(), ctypes.c_uint64()
+    st = lib.cess_rsa_parse_key(_buf(der), len(der), fmt, out, 512, ctypes.byref(ln), ctypes.byref(e))
+    if st != 0:
+        raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
+    return bytes(out)[: ln.value], e.value
 
 
 def comm_id() -> bytes:

@@ -8,6 +8,8 @@
 // Without a usable HIP device, cess_bls_ctx_create fails with CESS_BLS_E_NO_DEVICE.
 #include "host.hpp"
 
+#include <stdlib.h>
+
 #include "bls/consts.hpp"
 
 using namespace cess_host;
@@ -30,6 +32,7 @@ extern "C" const char* cess_bls_status_string(int s) {
     case CESS_BLS_E_BAD_KEY: return "public key does not deserialize (verify_bls would panic)";
     case CESS_BLS_E_BAD_SIG: return "signature does not deserialize (verify_bls would panic)";
     case CESS_BLS_E_NO_COMM: return "no communicator (cess_bls_comm_init)";
+    case CESS_RSA_E_UNSUPPORTED: return "RSA modulus longer than 2048 bits (not supported on the GPU)";
   }
   return "unknown status";
 }
@@ -67,17 +70,32 @@ void shard_of(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end, 
 }  // namespace cess_host
 
 static int alloc_stage(cess_bls_ctx* c) {
-  uint64_t n = c->cap;
+  const uint64_t n = c->cap, q = c->qcap;
   int r = CESS_BLS_OK;
   r |= c->pre.ensure(n);
   r |= c->code.ensure(n);
-  r |= c->inf.ensure(n);
-  r |= c->sig_aff.ensure(n * CESS_W_G1 * 4);
-  r |= c->h_aff.ensure(n * CESS_W_G1 * 4);
-  r |= c->fval.ensure(n * CESS_W_FP12 * 4);
-  r |= c->fe_slots.ensure(n * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
   r |= c->bitmap.ensure((n / 64 + 1) * 8);
+  r |= c->fval.ensure(q * CESS_W_FP12 * 4);
+  r |= c->fe_slots.ensure(q * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
+  for (int k = 0; k < (q < n ? 2 : 1); k++) {
+    r |= c->slot[k].inf.ensure(q);
+    r |= c->slot[k].sig_aff.ensure(q * CESS_W_G1 * 4);
+    r |= c->slot[k].h_aff.ensure(q * CESS_W_G1 * 4);
+  }
   return r ? CESS_BLS_E_OOM : CESS_BLS_OK;
+}
+
+// records per kernel launch: the whole chunk by default.  Pipelining parts of
+// 2^17-2^19 records (light kernels of part i+1 beside k_miller of part i) was
+// measured SLOWER on MI355X (1.970 M sigs/s unpipelined vs 1.914 / 1.873 /
+// 1.879 M at 512K / 256K / 128K parts, profiles/r02c_sweep_launch_records.txt:
+// k_miller slows from 187 to 263 ms per 1 M when co-resident waves share its
+// SIMDs), so the mechanism stays available via CESS_BLS_LAUNCH_RECORDS only.
+static uint64_t launch_records(uint64_t cap) {
+  uint64_t q = cap;
+  if (const char* e = getenv("CESS_BLS_LAUNCH_RECORDS")) q = strtoull(e, nullptr, 10);
+  q = std::max<uint64_t>(256, q & ~255ull);
+  return std::min(cap, q);
 }
 
 int cess_multi_create(const cess_bls_config* cfg, int ndev, cess_bls_ctx* c);   // host_multi.cpp
@@ -106,10 +124,18 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
   }
   uint64_t cap = (cfg && cfg->max_batch) ? cfg->max_batch : (1ull << 20);
   c->cap = (cap + 63) & ~63ull;
+  c->qcap = launch_records(c->cap);
   c->flags = cfg ? cfg->flags : 0;
   c->mode = cfg ? cfg->mode : CESS_BLS_MODE_PER_SIG;
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
+  bool ok = hipSetDevice(c->device) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; k < 2 && ok; k++)
+    ok = hipEventCreateWithFlags(&c->ev_light[k], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_mill[k], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
     cess_bls_ctx_destroy(c);
     return CESS_BLS_E_HIP;
   }
@@ -119,11 +145,6 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
     cess_bls_ctx_destroy(c);
     return r;
   }
-  for (int i = 0; i <= ST_N; i++)
-    if (hipEventCreate(&c->ev[i]) != hipSuccess) {
-      cess_bls_ctx_destroy(c);
-      return CESS_BLS_E_HIP;
-    }
   // G2PREPARED_NEG_G: prepare -G2 on the device with the same kernel (n = 1, stride = 1)
   uint32_t aff[48];
   {
@@ -163,59 +184,139 @@ extern "C" void cess_bls_ctx_destroy(cess_bls_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
   }
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  for (int i = 0; i <= ST_N; i++)
-    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+  for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {c->done_ev, c->ev_start, c->ev_light[0], c->ev_light[1], c->ev_mill[0], c->ev_mill[1]})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c->rlc;
+  cess_rsa_state_free(c);
   delete c;
+}
+
+int cess_host::prof_begin(cess_bls_ctx* c, hipStream_t s, int stage, hipEvent_t* a) {
+  (void)stage;
+  *a = nullptr;
+  if (!(c->flags & CESS_BLS_F_PROFILE)) return CESS_BLS_OK;
+  if (c->evused == c->evpool.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->evpool.push_back(e);
+  }
+  *a = c->evpool[c->evused++];
+  HIPCHK(hipEventRecord(*a, s));
+  return CESS_BLS_OK;
+}
+
+int cess_host::prof_end(cess_bls_ctx* c, hipStream_t s, int stage, hipEvent_t a) {
+  if (!a) return CESS_BLS_OK;
+  hipEvent_t b;
+  int r = prof_begin(c, s, stage, &b);
+  if (r) return r;
+  c->prof.push_back({stage, a, b});
+  return CESS_BLS_OK;
+}
+
+#define LAUNCH(stage, strm, ...)                        \
+  do {                                                  \
+    hipEvent_t pa_;                                     \
+    int pr_ = prof_begin(c, strm, stage, &pa_);         \
+    if (pr_) return pr_;                                \
+    hipLaunchKernelGGL(__VA_ARGS__);                    \
+    pr_ = prof_end(c, strm, stage, pa_);                \
+    if (pr_) return pr_;                                \
+  } while (0)
+
+// The pipeline over one chunk of n <= cap records, in parts of <= qcap.
+// light(S, q, off, m, strm) enqueues the part's decode/hash(/prepare) kernels
+// into stage slot S on strm; heavy(S, q, off, m) its Miller loop and final
+// exponentiation on the launch stream s.  One part runs on s alone; with
+// several, the light kernels run one part ahead on stream2 (slot = part % 2).
+template <class Light, class Heavy>
+static int pipeline(cess_bls_ctx* c, hipStream_t s, uint64_t n, Light&& light, Heavy&& heavy) {
+  const uint64_t q = c->qcap;
+  if (n <= q) {
+    int r = light(c->slot[0], q, (uint64_t)0, n, s);
+    if (r) return r;
+    return heavy(c->slot[0], q, (uint64_t)0, n);
+  }
+  hipStream_t s2 = c->stream2;
+  HIPCHK(hipEventRecord(c->ev_start, s));
+  HIPCHK(hipStreamWaitEvent(s2, c->ev_start, 0));
+  for (uint64_t off = 0, part = 0; off < n; off += q, part++) {
+    const uint64_t m = std::min(q, n - off);
+    const int k = (int)(part & 1);
+    StageSlot& S = c->slot[k];
+    if (part >= 2) HIPCHK(hipStreamWaitEvent(s2, c->ev_mill[k], 0));   // slot k free again
+    int r = light(S, q, off, m, s2);
+    if (r) return r;
+    HIPCHK(hipEventRecord(c->ev_light[k], s2));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_light[k], 0));
+    r = heavy(S, q, off, m);
+    if (r) return r;
+  }
+  return CESS_BLS_OK;
 }
 
 // Enqueue the verification pipeline for one chunk of n <= cap records.
 // sigs/pks/msgs/offs/codes/bitmap/pre are device pointers; gt (optional).
+// offs are rebased to msgs; bitmap word 0 covers record 0 of the chunk.
 int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* sigs, const uint8_t* pks,
                          const uint8_t* msgs, const uint64_t* offs, const uint8_t* pre, uint8_t* codes,
                          uint64_t* bitmap, uint8_t* gt) {
-  const uint64_t st = c->cap;
   // per-record key buffers (19.6 KB of line coefficients per signature) are
   // allocated on first use: keyed batches never touch them
-  if (c->pk_aff.ensure(st * CESS_W_G2 * 4) | c->coeffs.ensure(st * (uint64_t)CESS_W_COEFFS * 4)) return CESS_BLS_E_OOM;
-  const bool prof = (c->flags & CESS_BLS_F_PROFILE) != 0;
+  for (int k = 0; k < (n > c->qcap ? 2 : 1); k++)
+    if (c->slot[k].inf.ensure(c->qcap) | c->slot[k].sig_aff.ensure(c->qcap * CESS_W_G1 * 4) |
+        c->slot[k].h_aff.ensure(c->qcap * CESS_W_G1 * 4) | c->slot[k].pk_aff.ensure(c->qcap * CESS_W_G2 * 4) |
+        c->slot[k].coeffs.ensure(c->qcap * (uint64_t)CESS_W_COEFFS * 4))
+      return CESS_BLS_E_OOM;
   const uint32_t strict = (c->flags & CESS_BLS_F_STRICT_IDENTITY) ? 1u : 0u;
-  const unsigned g = grid_for(n);
-  uint8_t* inf = c->inf.as<uint8_t>();
-  if (prof) HIPCHK(hipEventRecord(c->ev[0], s));
-  hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, n, sigs, pre, codes, inf, c->sig_aff.as<uint32_t>(), st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[1], s));
-  hipLaunchKernelGGL(k_decode_pk, dim3(g), dim3(kBlock), 0, s, n, pks, pre, codes, inf, c->pk_aff.as<uint32_t>(), st,
-                     strict);
-  if (prof) HIPCHK(hipEventRecord(c->ev[2], s));
-  hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes, c->h_aff.as<uint32_t>(), st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[3], s));
-  hipLaunchKernelGGL(k_prepare, dim3(g), dim3(kBlock), 0, s, n, (const uint32_t*)c->pk_aff.as<uint32_t>(),
-                     c->coeffs.as<uint4>(), st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[4], s));
-  hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
-                     (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
-                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)c->coeffs.as<uint4>(),
-                     c->fval.as<uint4>(), c->fe_slots.as<uint4>(), st, (const uint32_t*)nullptr, st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
-  hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,
-                     gt, st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[6], s));
-  HIPCHK(hipGetLastError());
-  return CESS_BLS_OK;
+  auto light = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m, hipStream_t t) -> int {
+    const unsigned g = grid_for(m);
+    uint8_t* inf = S.inf.as<uint8_t>();
+    const uint8_t* p = pre ? pre + off : nullptr;
+    LAUNCH(ST_DECODE_SIG, t, k_decode_sig, dim3(g), dim3(kBlock), 0, t, m, sigs + 48 * off, p, codes + off, inf,
+           S.sig_aff.as<uint32_t>(), q);
+    LAUNCH(ST_DECODE_PK, t, k_decode_pk, dim3(g), dim3(kBlock), 0, t, m, pks + 96 * off, p, codes + off, inf,
+           S.pk_aff.as<uint32_t>(), q, strict);
+    LAUNCH(ST_HASH, t, k_hash, dim3(g), dim3(kBlock), 0, t, m, msgs, offs + off, (const uint8_t*)(codes + off),
+           S.h_aff.as<uint32_t>(), q);
+    LAUNCH(ST_PREPARE, t, k_prepare, dim3(g), dim3(kBlock), 0, t, m, (const uint32_t*)S.pk_aff.as<uint32_t>(),
+           S.coeffs.as<uint4>(), q);
+    HIPCHK(hipGetLastError());
+    return CESS_BLS_OK;
+  };
+  auto heavy = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m) -> int {
+    const unsigned g = grid_for(m);
+    LAUNCH(ST_MILLER, s, k_miller, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
+           (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
+           (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
+           (const uint4*)S.coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q,
+           (const uint32_t*)nullptr, q);
+    if (n > c->qcap) HIPCHK(hipEventRecord(c->ev_mill[(off / c->qcap) & 1], s));
+    LAUNCH(ST_FINAL, s, k_final, dim3(g), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
+           c->fe_slots.as<uint4>(), bitmap + off / 64, gt ? gt + 576 * off : (uint8_t*)nullptr, q);
+    HIPCHK(hipGetLastError());
+    return CESS_BLS_OK;
+  };
+  return pipeline(c, s, n, light, heavy);
 }
 
 int cess_host::collect_profile(cess_bls_ctx* c, hipStream_t s) {
   if (!(c->flags & CESS_BLS_F_PROFILE)) return CESS_BLS_OK;
   HIPCHK(hipStreamSynchronize(s));
-  for (int i = 0; i < ST_N; i++) {
+  HIPCHK(hipStreamSynchronize(c->stream2));
+  for (const ProfRec& p : c->prof) {
     float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
-    c->stage_ms[i] += ms;
+    HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+    c->stage_ms[p.stage] += ms;
+    c->stage_launches[p.stage]++;
   }
+  c->prof.clear();
+  c->evused = 0;
   return CESS_BLS_OK;
 }
 
@@ -445,30 +546,36 @@ extern "C" int cess_bls_keys_load(cess_bls_ctx* c, size_t k, const uint8_t* pks,
 // Miller loop over the table's coefficient rows, final exponentiation.
 static int run_chunk_keyed(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* sigs, const uint32_t* idx,
                            const uint8_t* msgs, const uint64_t* offs, uint8_t* codes, uint64_t* bitmap) {
-  const uint64_t st = c->cap;
-  const bool prof = (c->flags & CESS_BLS_F_PROFILE) != 0;
-  const unsigned g = grid_for(n);
-  uint8_t* inf = c->inf.as<uint8_t>();
-  if (prof) HIPCHK(hipEventRecord(c->ev[0], s));
-  hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, n, sigs, (const uint8_t*)nullptr, codes, inf,
-                     c->sig_aff.as<uint32_t>(), st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[1], s));
-  hipLaunchKernelGGL(k_merge_pk, dim3(g), dim3(kBlock), 0, s, n, idx, c->nkeys, (const uint8_t*)c->key_code.as<uint8_t>(),
-                     (const uint8_t*)c->key_inf.as<uint8_t>(), codes, inf);
-  if (prof) HIPCHK(hipEventRecord(c->ev[2], s));
-  hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes, c->h_aff.as<uint32_t>(), st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[3], s));
-  if (prof) HIPCHK(hipEventRecord(c->ev[4], s));
-  hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
-                     (const uint32_t*)c->sig_aff.as<uint32_t>(), (const uint32_t*)c->h_aff.as<uint32_t>(),
-                     (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)c->key_coeffs.as<uint4>(),
-                     c->fval.as<uint4>(), c->fe_slots.as<uint4>(), st, idx, (uint64_t)c->nkeys);
-  if (prof) HIPCHK(hipEventRecord(c->ev[5], s));
-  hipLaunchKernelGGL(k_final, dim3(g), dim3(kBlock), 0, s, n, codes, c->fval.as<uint4>(), c->fe_slots.as<uint4>(), bitmap,
-                     (uint8_t*)nullptr, st);
-  if (prof) HIPCHK(hipEventRecord(c->ev[6], s));
-  HIPCHK(hipGetLastError());
-  return CESS_BLS_OK;
+  for (int k = 0; k < (n > c->qcap ? 2 : 1); k++)
+    if (c->slot[k].inf.ensure(c->qcap) | c->slot[k].sig_aff.ensure(c->qcap * CESS_W_G1 * 4) |
+        c->slot[k].h_aff.ensure(c->qcap * CESS_W_G1 * 4))
+      return CESS_BLS_E_OOM;
+  auto light = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m, hipStream_t t) -> int {
+    const unsigned g = grid_for(m);
+    uint8_t* inf = S.inf.as<uint8_t>();
+    LAUNCH(ST_DECODE_SIG, t, k_decode_sig, dim3(g), dim3(kBlock), 0, t, m, sigs + 48 * off, (const uint8_t*)nullptr,
+           codes + off, inf, S.sig_aff.as<uint32_t>(), q);
+    LAUNCH(ST_DECODE_PK, t, k_merge_pk, dim3(g), dim3(kBlock), 0, t, m, idx + off, c->nkeys,
+           (const uint8_t*)c->key_code.as<uint8_t>(), (const uint8_t*)c->key_inf.as<uint8_t>(), codes + off, inf);
+    LAUNCH(ST_HASH, t, k_hash, dim3(g), dim3(kBlock), 0, t, m, msgs, offs + off, (const uint8_t*)(codes + off),
+           S.h_aff.as<uint32_t>(), q);
+    HIPCHK(hipGetLastError());
+    return CESS_BLS_OK;
+  };
+  auto heavy = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m) -> int {
+    const unsigned g = grid_for(m);
+    LAUNCH(ST_MILLER, s, k_miller, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
+           (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
+           (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
+           (const uint4*)c->key_coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q, idx + off,
+           (uint64_t)c->nkeys);
+    if (n > c->qcap) HIPCHK(hipEventRecord(c->ev_mill[(off / c->qcap) & 1], s));
+    LAUNCH(ST_FINAL, s, k_final, dim3(g), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
+           c->fe_slots.as<uint4>(), bitmap + off / 64, (uint8_t*)nullptr, q);
+    HIPCHK(hipGetLastError());
+    return CESS_BLS_OK;
+  };
+  return pipeline(c, s, n, light, heavy);
 }
 
 extern "C" int cess_bls_verify_batch_keyed_device(cess_bls_ctx* c, size_t n, const uint8_t* d_sigs,
@@ -613,22 +720,31 @@ extern "C" int cess_bls_hash_to_g1_batch(cess_bls_ctx* c, size_t n, const uint8_
   return gen_batch(c, 2, n, nullptr, msgs, offs, out48);
 }
 
-extern "C" int cess_bls_stage_times(cess_bls_ctx* c, const char** names, double* ms, int max, int reset) {
+extern "C" int cess_bls_stage_stats(cess_bls_ctx* c, const char** names, double* ms, uint64_t* launches, int max,
+                                    int reset) {
   ENTRY(c);
   int k = std::min(max, (int)ST_N);
   for (int i = 0; i < k; i++) {
     double v = c->stage_ms[i];
-    for (cess_bls_ctx* s : c->subs) v += s->stage_ms[i];
+    uint64_t l = c->stage_launches[i];
+    for (cess_bls_ctx* s : c->subs) v += s->stage_ms[i], l += s->stage_launches[i];
     if (names) names[i] = kStageNames[i];
     if (ms) ms[i] = v;
+    if (launches) launches[i] = l;
   }
   if (reset) {
-    for (int i = 0; i < ST_N; i++) c->stage_ms[i] = 0;
+    for (int i = 0; i < ST_N; i++) c->stage_ms[i] = 0, c->stage_launches[i] = 0;
     for (cess_bls_ctx* s : c->subs)
-      for (int i = 0; i < ST_N; i++) s->stage_ms[i] = 0;
+      for (int i = 0; i < ST_N; i++) s->stage_ms[i] = 0, s->stage_launches[i] = 0;
   }
   return ST_N;
 }
+
+extern "C" int cess_bls_stage_times(cess_bls_ctx* c, const char** names, double* ms, int max, int reset) {
+  return cess_bls_stage_stats(c, names, ms, nullptr, max, reset);
+}
+
+extern "C" uint64_t cess_bls_launch_records(cess_bls_ctx* c) { return c ? c->qcap : 0; }
 
 // device memory helpers -------------------------------------------------------
 extern "C" int cess_bls_device_alloc(cess_bls_ctx* c, size_t bytes, void** d_out) {

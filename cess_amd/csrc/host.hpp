@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/cess_bls.h"
+#include "../../include/cess_rsa.h"
 #include "kernels.hpp"
 
 // kernels (k_*.hip)
@@ -84,21 +85,46 @@ struct RlcState {
   DevBuf seg, part2, rec_coeffs, lists, d_gt_all;
 };
 
+// Stage buffers of one in-flight pipeline part (SoA, stride = qcap).
+struct StageSlot {
+  DevBuf inf, sig_aff, h_aff, pk_aff, coeffs;
+};
+
+// One profiled kernel launch: [a, b] events on the launch's stream.
+struct ProfRec {
+  int stage;
+  hipEvent_t a, b;
+};
+
 }  // namespace cess_host
+
+struct RsaState;   // host_rsa.cpp
+void cess_rsa_state_free(cess_bls_ctx* c);
 
 struct cess_bls_ctx {
   int device = 0;
-  uint64_t cap = 0;
+  uint64_t cap = 0;    // records per host-API chunk (staging buffers)
+  uint64_t qcap = 0;   // records per kernel launch (pipeline part; stage-buffer stride)
   uint32_t flags = 0;
   uint32_t mode = CESS_BLS_MODE_PER_SIG;
   hipStream_t stream = nullptr;
-  // stage buffers (SoA, stride = cap)
-  cess_host::DevBuf pre, code, inf, sig_aff, pk_aff, h_aff, coeffs, fval, fe_slots, bitmap, neg_g2;
+  // Pipeline (run_chunk): a chunk longer than qcap runs as parts; the light
+  // kernels of part i+1 (decode, hash, prepare: no LDS, 128 VGPRs) run on
+  // stream2 while k_miller of part i (one wave per SIMD: 144 KiB of LDS, 256
+  // VGPRs) runs on the launch stream, so they share the CUs' issue slots.
+  // Two stage slots alternate between parts.
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_start = nullptr, ev_light[2] = {}, ev_mill[2] = {};
+  cess_host::StageSlot slot[2];
+  cess_host::DevBuf pre, code, fval, fe_slots, bitmap, neg_g2;
   // staging for the host-buffer APIs
   cess_host::DevBuf in_sigs, in_pks, in_msgs, in_offs, out_gt, in_sks, out_bytes;
-  // profiling
-  hipEvent_t ev[cess_host::ST_N + 1] = {};
+  // profiling: per-launch events (pool reused after each collect)
+  std::vector<hipEvent_t> evpool;
+  size_t evused = 0;
+  std::vector<cess_host::ProfRec> prof;
   double stage_ms[cess_host::ST_N] = {};
+  uint64_t stage_launches[cess_host::ST_N] = {};
   cess_host::RlcState* rlc = nullptr;
   // distinct-key table (cess_bls_keys_load): decoded keys + G2Prepared rows, stride = nkeys
   uint32_t nkeys = 0;
@@ -118,6 +144,8 @@ struct cess_bls_ctx {
   // multi-device context (cess_bls_config.n_devices > 1): one sub-context per
   // device, batches sharded by index across them from host threads
   std::vector<cess_bls_ctx*> subs;
+  // RSA PKCS#1 v1.5 key tables and staging (host_rsa.cpp)
+  RsaState* rsa = nullptr;
 };
 
 #define HIPCHK(x)                                 \
@@ -140,6 +168,9 @@ int order_begin(cess_bls_ctx* c, hipStream_t s);
 // record the end of this call's work on s
 int order_end(cess_bls_ctx* c, hipStream_t s);
 
+// profiling brackets around one launch on stream s (no-ops without CESS_BLS_F_PROFILE)
+int prof_begin(cess_bls_ctx* c, hipStream_t s, int stage, hipEvent_t* a);
+int prof_end(cess_bls_ctx* c, hipStream_t s, int stage, hipEvent_t a);
 int run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
               const uint64_t* offs, const uint8_t* pre, uint8_t* codes, uint64_t* bitmap, uint8_t* gt);
 int verify_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,

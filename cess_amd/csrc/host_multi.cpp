@@ -355,3 +355,16 @@ int cess_multi_gt(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t*
                        codes_out ? codes_out + b : nullptr, nullptr, gt_out + 576 * b);
   });
 }
+
+int cess_rsa_one(cess_bls_ctx* s, size_t n, const uint32_t* key_idx, const uint8_t* sigs, const uint64_t* soffs,
+                 const uint8_t* msgs, const uint64_t* moffs, uint8_t* codes_out, uint64_t* bitmap_out);
+
+int cess_multi_rsa(cess_bls_ctx* c, size_t n, const uint32_t* key_idx, const uint8_t* sigs, const uint64_t* soffs,
+                   const uint8_t* msgs, const uint64_t* moffs, uint8_t* codes_out, uint64_t* bitmap_out) {
+  if (n == 0) return CESS_BLS_OK;
+  if (!key_idx || !soffs || !moffs) return CESS_BLS_E_INVALID_ARG;
+  return for_each_shard(c, n, [&](cess_bls_ctx* s, uint64_t b, uint64_t e) {
+    return cess_rsa_one(s, e - b, key_idx + b, sigs, soffs + b, msgs, moffs + b, codes_out ? codes_out + b : nullptr,
+                        bitmap_out ? bitmap_out + b / 64 : nullptr);
+  });
+}

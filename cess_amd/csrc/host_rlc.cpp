@@ -272,8 +272,8 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   //    (signature first, :244-245), hash_to_g1 (:25-31), P_i = r_i sig_i, Q_i = r_i H_i
   std::vector<uint8_t> hc, hi;
   std::vector<uint64_t> rebased;
-  for (uint64_t off = 0; off < n; off += c->cap) {
-    const uint64_t m = std::min<uint64_t>(c->cap, n - off);
+  for (uint64_t off = 0; off < n; off += c->qcap) {
+    const uint64_t m = std::min<uint64_t>(c->qcap, n - off);
     const uint64_t mb0 = offs[off], mb1 = offs[off + m];
     if (mb1 < mb0) return CESS_BLS_E_INVALID_ARG;
     rebased.resize(m + 1);
@@ -287,13 +287,14 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
     const unsigned g = grid_for(m);
+    StageSlot& S = c->slot[0];
     hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
-                       c->code.as<uint8_t>(), c->inf.as<uint8_t>(), c->sig_aff.as<uint32_t>(), c->cap);
+                       c->code.as<uint8_t>(), S.inf.as<uint8_t>(), S.sig_aff.as<uint32_t>(), c->qcap);
     HIPCHK(hipGetLastError());
     hc.resize(m);
     hi.resize(m);
     HIPCHK(hipMemcpyAsync(hc.data(), c->code.p, m, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hi.data(), c->inf.p, m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hi.data(), S.inf.p, m, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     for (uint64_t j = 0; j < m; j++) {
       if (hc[j] != 0) continue;
@@ -303,13 +304,13 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     }
     memcpy(&R.codes[off], hc.data(), m);
     HIPCHK(hipMemcpyAsync(c->code.p, hc.data(), m, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->inf.p, hi.data(), m, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(S.inf.p, hi.data(), m, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
-                       (const uint8_t*)c->code.as<uint8_t>(), c->h_aff.as<uint32_t>(), c->cap);
+                       (const uint8_t*)c->code.as<uint8_t>(), S.h_aff.as<uint32_t>(), c->qcap);
     hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)c->code.as<uint8_t>(),
-                       (const uint8_t*)c->inf.as<uint8_t>(), (const uint32_t*)c->sig_aff.as<uint32_t>(),
-                       (const uint32_t*)c->h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(),
-                       index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->cap, (uint64_t)n);
+                       (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
+                       (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(),
+                       index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->qcap, (uint64_t)n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // hc/hi are reused by the next chunk
   }

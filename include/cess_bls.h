@@ -269,6 +269,16 @@ int cess_bls_enclave_verify_bls(cess_bls_ctx* ctx, const uint8_t* key, size_t ke
 /* Per-stage timings (ms, summed since the last reset) when CESS_BLS_F_PROFILE is
  * set.  names/ms arrays of length max; returns the number of stages. */
 int cess_bls_stage_times(cess_bls_ctx* ctx, const char** names, double* ms, int max, int reset);
+/* As cess_bls_stage_times, plus the number of kernel launches per stage
+ * (launches may be NULL).  Each launch is bracketed by events on the stream it
+ * runs on, so a stage's time is the sum of its own launch durations even when
+ * the pipeline overlaps stages of different parts. */
+int cess_bls_stage_stats(cess_bls_ctx* ctx, const char** names, double* ms, uint64_t* launches, int max, int reset);
+/* Records per kernel launch (pipeline part): batches longer than this run as
+ * parts whose decode/hash/prepare kernels overlap the previous part's Miller
+ * loop on a second stream.  Default: max_batch (no overlap; overlap measured
+ * slower on MI355X); env CESS_BLS_LAUNCH_RECORDS. */
+uint64_t cess_bls_launch_records(cess_bls_ctx* ctx);
 
 const char* cess_bls_status_string(int status);
 const char* cess_bls_version(void);

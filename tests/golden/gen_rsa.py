@@ -1,0 +1,97 @@
+"""Generate tests/golden/rsa_vectors.json from the RSA oracle (oracle/rsa_oracle.py).
+
+Deterministic (seeded) keys of 1024 / 2048 / 3072 bits, e = 65537 and e = 3,
+each as SPKI DER (what cp_enclave_verify::verify_rsa parses) and PKCS#1 DER
+(Podr2Key = [u8; 270], primitives/common/src/lib.rs:54), with valid and
+invalid raw PKCS#1 v1.5 signatures (Pkcs1v15Sign::new_raw()) -- including the
+reference test's own message "hello world!" (enclave-verify/src/lib.rs:248) --
+plus malformed DER keys.  Parity is UNPINNED (see the oracle's header).
+
+Usage: python tests/golden/gen_rsa.py
+"""
+import json
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+from oracle import rsa_oracle as o  # noqa: E402
+
+
+def main():
+    rng = random.Random(0x525341)
+    keys = []
+    for bits, e in ((2048, 65537), (2048, 65537), (1024, 65537), (3072, 65537), (2048, 3)):
+        n, e, d = o.gen_key(bits, e, rng)
+        keys.append({"n": n, "e": e, "d": d})
+    out_keys = [{"bits": k["n"].bit_length(), "e": k["e"], "spki": o.encode_spki(k["n"], k["e"]).hex(),
+                 "pkcs1": o.encode_pkcs1(k["n"], k["e"]).hex()} for k in keys]
+    cases = []
+
+    def add(name, ki, msg, sig):
+        k = keys[ki]
+        cases.append({"name": name, "key": ki, "msg": msg.hex(), "sig": sig.hex(),
+                      "code": o.verify_code(k["n"], k["e"], msg, sig)})
+
+    for ki, k in enumerate(keys):
+        n, d = k["n"], k["d"]
+        kb = (n.bit_length() + 7) // 8
+        hw = b"hello world!"                                 # the reference test's message
+        add(f"k{ki}_hello_world", ki, hw, o.sign_raw(n, d, hw))
+        for j in range(3):
+            m = bytes(rng.randrange(256) for _ in range(32))
+            add(f"k{ki}_valid32_{j}", ki, m, o.sign_raw(n, d, m))
+        add(f"k{ki}_empty_msg", ki, b"", o.sign_raw(n, d, b""))
+        mx = bytes(rng.randrange(256) for _ in range(kb - 11))
+        add(f"k{ki}_max_msg", ki, mx, o.sign_raw(n, d, mx))
+        s = o.sign_raw(n, d, hw)
+        add(f"k{ki}_wrong_msg", ki, b"hello world?", s)
+        add(f"k{ki}_flipped_sig", ki, hw, s[:-1] + bytes([s[-1] ^ 1]))
+        add(f"k{ki}_short_sig", ki, hw, s[1:])
+        add(f"k{ki}_long_sig", ki, hw, b"\x00" + s)
+        add(f"k{ki}_sig_eq_n", ki, hw, n.to_bytes(kb, "big"))
+        add(f"k{ki}_sig_max", ki, hw, b"\xff" * kb)
+        add(f"k{ki}_sig_zero", ki, hw, bytes(kb))
+        add(f"k{ki}_sig_one", ki, b"", (1).to_bytes(kb, "big"))
+        add(f"k{ki}_msg_too_long", ki, bytes(kb - 10), s)
+        # wrong block type (0x02) and a missing separator, both validly exponentiated
+        for nm, em in (("bt02", b"\x00\x02" + b"\xff" * (kb - len(hw) - 3) + b"\x00" + hw),
+                       ("nosep", b"\x00\x01" + b"\xff" * (kb - len(hw) - 2) + hw),
+                       ("short_ps", b"\x00\x01" + b"\xff" * 7 + b"\x00" + bytes(kb - 10))):
+            add(f"k{ki}_{nm}", ki, hw if nm != "short_ps" else bytes(kb - 10),
+                pow(int.from_bytes(em, "big"), d, n).to_bytes(kb, "big"))
+    # malformed keys (verify_rsa panics: PublicKey::from_public_key_der(..).unwrap())
+    good = bytes.fromhex(out_keys[0]["spki"])
+    bad_keys = [{"name": "truncated", "der": good[:-1].hex()},
+                {"name": "trailing", "der": (good + b"\x00").hex()},
+                {"name": "wrong_oid", "der": good.replace(o.RSA_OID, bytes.fromhex("2a8648ce3d0201")).hex()},
+                {"name": "pkcs1_not_spki", "der": out_keys[0]["pkcs1"]},
+                {"name": "even_modulus", "der": o.encode_spki(keys[0]["n"] + 1, 65537).hex()},
+                {"name": "e_one", "der": o.encode_spki(keys[0]["n"], 1).hex()},
+                {"name": "empty", "der": ""}]
+    for b in bad_keys:
+        try:
+            o.parse_spki(bytes.fromhex(b["der"]))
+            b["parses"] = True
+        except o.KeyError_:
+            b["parses"] = False
+    assert not any(b["parses"] for b in bad_keys)
+    # bench pool (bench.py --mode rsa): valid raw signatures over 32-byte
+    # messages under key 0 (2048-bit), replicated by the bench to its batch size
+    n0, d0 = keys[0]["n"], keys[0]["d"]
+    pool = []
+    for _ in range(256):
+        m = bytes(rng.randrange(256) for _ in range(32))
+        pool.append({"msg": m.hex(), "sig": o.sign_raw(n0, d0, m).hex()})
+    doc = {"generator": "tests/golden/gen_rsa.py (oracle/rsa_oracle.py)",
+           "codes": {"0": "OK", "1": "SIG_LEN", "2": "SIG_RANGE", "3": "MSG_LEN", "4": "MISMATCH"},
+           "keys": out_keys, "cases": cases, "bad_keys": bad_keys, "bench_pool_key0": pool}
+    with open(os.path.join(ROOT, "tests", "golden", "rsa_vectors.json"), "w") as f:
+        json.dump(doc, f, indent=1)
+    print(len(cases), "cases,", len(bad_keys), "bad keys")
+
+
+if __name__ == "__main__":
+    main()

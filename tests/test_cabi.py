@@ -12,9 +12,11 @@ LIB = os.path.join(ROOT, "cess_amd", "lib", "libcess_bls.so")
 
 
 def header_symbols():
-    with open(os.path.join(ROOT, "include", "cess_bls.h")) as f:
-        txt = f.read()
-    return sorted(set(re.findall(r"\b(cess_bls_[a-z0-9_]+)\s*\(", txt)))
+    txt = ""
+    for h in ("cess_bls.h", "cess_rsa.h"):
+        with open(os.path.join(ROOT, "include", h)) as f:
+            txt += f.read()
+    return sorted(set(re.findall(r"\b(cess_(?:bls|rsa)_[a-z0-9_]+)\s*\(", txt)))
 
 
 @pytest.fixture(scope="module")

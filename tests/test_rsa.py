@@ -1,0 +1,158 @@
+"""RSA PKCS#1 v1.5 raw verify (cp_enclave_verify::verify_rsa,
+/root/reference/primitives/enclave-verify/src/lib.rs:221-228).
+
+CPU: the oracle (oracle/rsa_oracle.py) reproduces every committed fixture
+(tests/golden/rsa_vectors.json) and the reference test's round trip
+(`cryptos_rsa`, enclave-verify/src/lib.rs:242-255: sign "hello world!" with
+Pkcs1v15Sign::new_raw(), verify -> true); the library's host-side DER parser
+agrees with the oracle on every good and malformed key.  Parity is unpinned
+(no fixed vector in the reference; the rsa crate cannot run here).
+
+GPU: per-record codes of the batch kernel equal the fixture codes through the
+host-buffer, device-resident and verify_rsa entry points."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import rsa_oracle as o
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def rv():
+    with open(os.path.join(ROOT, "tests", "golden", "rsa_vectors.json")) as f:
+        return json.load(f)
+
+
+def _key(rv, ki):
+    return o.parse_spki(bytes.fromhex(rv["keys"][ki]["spki"]))
+
+
+def test_oracle_matches_fixtures(rv):
+    for c in rv["cases"]:
+        n, e = _key(rv, c["key"])
+        assert o.verify_code(n, e, bytes.fromhex(c["msg"]), bytes.fromhex(c["sig"])) == c["code"], c["name"]
+    for b in rv["bad_keys"]:
+        with pytest.raises(o.KeyError_):
+            o.parse_spki(bytes.fromhex(b["der"]))
+
+
+def test_reference_round_trip():
+    """enclave-verify/src/lib.rs:242-255 with a fixed-seed key."""
+    n, e, d = o.gen_key(1024, 65537, random.Random(7))
+    doc = o.encode_spki(n, e)
+    sig = o.sign_raw(n, d, b"hello world!")
+    assert o.verify_rsa(doc, b"hello world!", sig) is True
+    assert o.verify_rsa(doc, b"hello world?", sig) is False
+    assert o.parse_pkcs1(o.encode_pkcs1(n, e)) == (n, e)
+
+
+def test_host_der_parser_matches_oracle(rv):
+    from cess_amd import bls
+    for k in rv["keys"]:
+        n, e = o.parse_spki(bytes.fromhex(k["spki"]))
+        mod, ee = bls.rsa_parse_key(bytes.fromhex(k["spki"]), bls.RSA_KEY_SPKI)
+        assert int.from_bytes(mod, "big") == n and ee == e
+        mod, ee = bls.rsa_parse_key(bytes.fromhex(k["pkcs1"]), bls.RSA_KEY_PKCS1)
+        assert int.from_bytes(mod, "big") == n and ee == e
+    assert len(bytes.fromhex(rv["keys"][0]["pkcs1"])) == 270          # Podr2Key = [u8; 270]
+    for b in rv["bad_keys"]:
+        with pytest.raises(bls.BlsInfraError) as ei:
+            bls.rsa_parse_key(bytes.fromhex(b["der"]), bls.RSA_KEY_SPKI)
+        assert ei.value.status == bls.E_BAD_KEY, b["name"]
+
+
+def _gpu_ctx():
+    from cess_amd import bls
+    return bls.Context(max_batch=4096)
+
+
+@pytest.mark.gpu
+def test_gpu_fixture_codes(rv):
+    from cess_amd import bls
+    c = _gpu_ctx()
+    try:
+        st = c.rsa_keys_load([bytes.fromhex(k["spki"]) for k in rv["keys"]])
+        # 1024 / 2048-bit keys load; the 3072-bit key is beyond the GPU size classes
+        assert st == [0 if k["bits"] <= 2048 else bls.RSA_E_UNSUPPORTED for k in rv["keys"]]
+        cases = rv["cases"]
+        codes = c.rsa_verify_batch([x["key"] for x in cases], [bytes.fromhex(x["msg"]) for x in cases],
+                                   [bytes.fromhex(x["sig"]) for x in cases])
+        for x, got in zip(cases, codes):
+            bits = rv["keys"][x["key"]]["bits"]
+            assert got == (x["code"] if bits <= 2048 else 5), x["name"]
+        # the PKCS#1 (Podr2Key) encoding gives the same table
+        assert c.rsa_keys_load([bytes.fromhex(k["pkcs1"]) for k in rv["keys"]], bls.RSA_KEY_PKCS1)[:3] == [0, 0, 0]
+        sel = [x for x in cases if rv["keys"][x["key"]]["bits"] <= 2048]
+        assert c.rsa_verify_batch([x["key"] for x in sel], [bytes.fromhex(x["msg"]) for x in sel],
+                                  [bytes.fromhex(x["sig"]) for x in sel]) == bytes(x["code"] for x in sel)
+        # out-of-range key index -> KEY
+        assert c.rsa_verify_batch([9], [b"x"], [bytes(256)]) == bytes([5])
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_verify_rsa_dropin(rv):
+    from cess_amd import bls
+    c = _gpu_ctx()
+    try:
+        for x in rv["cases"]:
+            k = rv["keys"][x["key"]]
+            der, msg, sig = bytes.fromhex(k["spki"]), bytes.fromhex(x["msg"]), bytes.fromhex(x["sig"])
+            if k["bits"] > 2048:
+                with pytest.raises(bls.BlsInfraError) as ei:
+                    c.verify_rsa(der, msg, sig)
+                assert ei.value.status == bls.RSA_E_UNSUPPORTED
+                continue
+            assert c.verify_rsa(der, msg, sig) == (x["code"] == 0), x["name"]
+        for b in rv["bad_keys"]:
+            with pytest.raises(bls.BlsInfraError) as ei:
+                c.verify_rsa(bytes.fromhex(b["der"]), b"hello world!", bytes(256))
+            assert ei.value.status == bls.E_BAD_KEY
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_device_batch_many(rv):
+    """A few thousand records (random valid/invalid mix over the 2048/1024-bit
+    keys) through the device-resident entry point: codes equal the oracle's."""
+    from cess_amd import bls
+    rng = random.Random(11)
+    keys = [k for k in rv["keys"] if k["bits"] <= 2048]
+    parsed = [o.parse_spki(bytes.fromhex(k["spki"])) for k in keys]
+    base = [x for x in rv["cases"] if rv["keys"][x["key"]]["bits"] <= 2048]
+    kmap = {rv["keys"].index(k): j for j, k in enumerate(keys)}
+    recs = []
+    for _ in range(3000):
+        x = rng.choice(base)
+        msg, sig = bytes.fromhex(x["msg"]), bytes.fromhex(x["sig"])
+        if rng.random() < 0.3 and sig:
+            sig = sig[:-1] + bytes([sig[-1] ^ rng.randrange(1, 256)])
+        kj = kmap[x["key"]]
+        n, e = parsed[kj]
+        recs.append((kj, msg, sig, o.verify_code(n, e, msg, sig)))
+    c = _gpu_ctx()
+    try:
+        c.rsa_keys_load([bytes.fromhex(k["spki"]) for k in keys])
+        S = b"".join(r[2] for r in recs)
+        M = b"".join(r[1] for r in recs)
+        so = np.cumsum([0] + [len(r[2]) for r in recs]).astype(np.uint64)
+        mo = np.cumsum([0] + [len(r[1]) for r in recs]).astype(np.uint64)
+        d = [c.to_device(np.array([r[0] for r in recs], dtype=np.uint32)), c.to_device(S), c.to_device(so),
+             c.to_device(M if M else b"\0"), c.to_device(mo)]
+        dc = c.device_alloc(len(recs))
+        c.rsa_verify_batch_device(len(recs), d[0], d[1], d[2], d[3], d[4], dc)
+        c.synchronize()
+        got = c.from_device(dc, len(recs))
+        for p in d + [dc]:
+            c.device_free(p)
+    finally:
+        c.close()
+    assert list(got) == [r[3] for r in recs]
+    assert 0 in got and 4 in got

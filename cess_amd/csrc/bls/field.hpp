@@ -33,7 +33,6 @@
 #else
 #include <hip/hip_runtime.h>
 #define CESS_HD __device__ __forceinline__
-#define CESS_NOINLINE __device__ __noinline__
 #define CESS_CONST static constexpr
 #endif
 
@@ -547,9 +546,6 @@ CESS_HD fp2 mul8(const fp2& a) { return {mul8(a.c0), mul8(a.c1)}; }
 //                       each column of t is exactly v0 + v1 + cross terms).
 // c0 < 2^770 < p 2^392, so each reduction returns < 2p.  3 x 196 product +
 // 2 x 196 reduction mads = 980 vs 1176 for three separate products.
-#ifndef CESS_KSQ_MUL
-#define CESS_KSQ_MUL mul_sep   // Fp2 product inside the compressed squaring
-#endif
 #ifndef CESS_FP2_MUL_LAZY
 #define CESS_FP2_MUL_LAZY 1
 #endif
@@ -802,46 +798,6 @@ CESS_HD fp12 cyclotomic_square(const fp12& f) {
   r.c0 = {z0, z4, z3};
   r.c1 = {z2, z1, z5};
   return r;
-}
-
-// Karabina compressed squaring in the cyclotomic subgroup (eprint 2010/542):
-// with Granger-Scott's naming z0 = c0.c0, z1 = c1.c1, z2 = c1.c0, z3 = c0.c2,
-// z4 = c0.c1, z5 = c1.c2, the square's (z2, z3, z4, z5) depend on (z2..z5)
-// only:  z2' = 2(z2 + 3 xi z4 z5),  z3' = 3(z4^2 + xi z5^2) - 2 z3,
-//        z4' = 3(z2^2 + xi z3^2) - 2 z4,  z5' = 2(z5 + 3 z2 z3),
-// with z4^2 + xi z5^2 = (z4 + z5)(z4 + xi z5) - (1 + xi) z4 z5 (same for z2, z3):
-// four Fp2 products per squaring instead of Granger-Scott's nine squarings.
-// (Mapping checked against the oracle's Fp12 squaring.)  z0, z1 are recovered
-// by cyc_decompress.
-CESS_HD fp2 mul_sep(const fp2& a, const fp2& b) {   // 3 separately reduced products (fewer registers)
-  const fp v0 = mul(a.c0, b.c0), v1 = mul(a.c1, b.c1);
-  const fp t = mul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1));
-  return {sub(v0, v1), sub(sub(t, v0), v1)};
-}
-CESS_HD void cyc_sqr_compressed(fp2& z2, fp2& z3, fp2& z4, fp2& z5) {
-  const fp2 b45 = CESS_KSQ_MUL(z4, z5);
-  const fp2 nb45 = mul_nr(b45);
-  const fp2 s45 = sub(sub(CESS_KSQ_MUL(add_nr(z4, z5), add_nr(z4, mul_nr(z5))), b45), nb45);
-  const fp2 b23 = CESS_KSQ_MUL(z2, z3);
-  const fp2 s23 = sub(sub(CESS_KSQ_MUL(add_nr(z2, z3), add_nr(z2, mul_nr(z3))), b23), mul_nr(b23));
-  z2 = dbl(add(z2, mul3(nb45)));
-  z3 = sub(mul3(s45), dbl(z3));
-  z4 = sub(mul3(s23), dbl(z4));
-  z5 = dbl(add(z5, mul3(b23)));
-}
-// numerator / denominator of z1 for a compressed cyclotomic element:
-//   z2 != 0: z1 = (xi z5^2 + 3 z4^2 - 2 z3) / (4 z2);  z2 == 0: z1 = 2 z4 z5 / z3.
-// den == 0 (z2 = z3 = 0, e.g. the identity) cannot be decompressed.
-CESS_HD void cyc_z1_frac(const fp2& z2, const fp2& z3, const fp2& z4, const fp2& z5, fp2& num, fp2& den) {
-  const bool a = !is_zero(z2);
-  const fp2 n0 = sub(add(mul_nr(sqr(z5)), mul3(sqr(z4))), dbl(z3));
-  const fp2 n1 = dbl(mul(z4, z5));
-  num = select(a, n0, n1);
-  den = select(a, dbl(dbl(z2)), z3);
-}
-// z0 = xi (2 z1^2 + z2 z5 - 3 z3 z4) + 1
-CESS_HD fp2 cyc_z0(const fp2& z1, const fp2& z2, const fp2& z3, const fp2& z4, const fp2& z5) {
-  return add(mul_nr(sub(add(dbl(sqr(z1)), mul(z2, z5)), mul3(mul(z3, z4)))), fp2_one());
 }
 
 // f^x for x = -0xd201000000010000 in the cyclotomic subgroup

@@ -121,11 +121,12 @@ CESS_HD fp12 miller_loop2(const g1a& pa, bool skip_a, const g1a& pb, bool skip_b
 }
 
 // ---------------------------------------------------------------------------
-// Final exponentiation.  The coarse Fp12 operations are out-of-line helpers
-// with pointer arguments so each exists once in the code object (instruction
-// cache / compile time); operands then live in per-lane scratch, which costs
-// far less than the 18-54 Fp multiplies each helper performs.
+// Value-based final exponentiation: HOST EMULATION ONLY (tests/hostemu: the
+// CPU baseline and an independent cross-check of the staged program the
+// k_final kernel runs, bls/staged.hpp).  Not compiled for the device, so no
+// out-of-line (__noinline__) device function exists in the product library.
 // ---------------------------------------------------------------------------
+#if defined(CESS_HOSTEMU)
 CESS_NOINLINE void fe_mul(fp12* r, const fp12* a, const fp12* b) { *r = mul(*a, *b); }
 CESS_NOINLINE void fe_cycsq(fp12* r, const fp12* a) { *r = cyclotomic_square(*a); }
 CESS_NOINLINE void fe_frob(fp12* r, const fp12* a, int k) {
@@ -186,5 +187,6 @@ CESS_HD fp12 final_exponentiation(const fp12& f) {
   fe_mul(&t3, &t3, &t4);
   return t3;
 }
+#endif  // CESS_HOSTEMU
 
 }  // namespace bls

@@ -219,68 +219,6 @@ CESS_HD void mul12_stream(const D& d, const S& f, const G& g, const T& t) {
               [&](int j, const fp2& x) { d.st(3 + j, sub(sub(x, t.ld(j)), d.ld(3 + j))); });
 }
 
-// d <- f^2 (complex squaring) with streamed operands; d distinct from f, t a
-// one-Fp6 temporary store.  ab = f0 f1 goes to t; d.c0 = (f0 + f1)(f0 + v f1)
-// - ab - v ab, d.c1 = 2 ab.
-template <class D, class S, class T>
-CESS_HD void sqr12_stream(const D& d, const S& f, const T& t) {
-  mul6_stream([&](int j) { return f.ld(j); }, [&](int j) { return f.ld(3 + j); },
-              [&](int j, const fp2& v) { t.st(j, v); });
-  mul6_stream([&](int j) { return add_nr(f.ld(j), f.ld(3 + j)); },
-              [&](int j) { return j == 0 ? add_nr(f.ld(0), mul_nr(f.ld(5))) : add_nr(f.ld(j), f.ld(2 + j)); },
-              [&](int j, const fp2& x) {
-                const fp2 vab = j == 0 ? mul_nr(t.ld(2)) : t.ld(j - 1);
-                d.st(j, sub(sub(x, t.ld(j)), vab));
-              });
-#pragma unroll 1
-  for (int j = 0; j < 3; j++) d.st(3 + j, dbl(t.ld(j)));
-}
-
-// d <- f * (c0 + c1 v + c4 v w) (Fp12::mul_by_014) with streamed operands; d
-// distinct from f, t a one-Fp6 temporary store.  bb = f1 c4 v goes to t,
-// d.c0 = aa + v bb with aa = f0 (c0 + c1 v), and d.c1 = (f0 + f1)(c0 + (c1 +
-// c4) v) - aa - bb, using aa = d.c0 - v bb.
-template <class D, class S, class T>
-CESS_HD void mul014_stream(const D& d, const S& f, const fp2& c0, const fp2& c1, const fp2& c4, const T& t) {
-  t.st(0, mul_nr(mul(f.ld(5), c4)));
-  CESS_MEMBAR();
-  t.st(1, mul(f.ld(3), c4));
-  CESS_MEMBAR();
-  t.st(2, mul(f.ld(4), c4));
-  CESS_MEMBAR();
-  {
-    const fp2 t0 = mul(f.ld(0), c0);
-    CESS_MEMBAR();
-    const fp2 t1 = mul(f.ld(1), c1);
-    CESS_MEMBAR();
-    d.st(1, add(sub(sub(mul(add_nr(f.ld(0), f.ld(1)), add_nr(c0, c1)), t0), t1), t.ld(0)));
-    CESS_MEMBAR();
-    d.st(0, add(add(mul_nr(mul(f.ld(2), c1)), t0), mul_nr(t.ld(2))));
-    CESS_MEMBAR();
-    d.st(2, add(add(mul(f.ld(2), c0), t1), t.ld(1)));
-    CESS_MEMBAR();
-  }
-  const fp2 e = add(c1, c4);
-  const fp2 u0 = mul(add_nr(f.ld(0), f.ld(3)), c0);
-  CESS_MEMBAR();
-  const fp2 u1 = mul(add_nr(f.ld(1), f.ld(4)), e);
-  CESS_MEMBAR();
-  {
-    const fp2 x = sub(sub(mul(add_nr(add_nr(f.ld(0), f.ld(3)), add_nr(f.ld(1), f.ld(4))), add_nr(c0, e)), u0), u1);
-    d.st(4, sub(add(sub(x, d.ld(1)), t.ld(0)), t.ld(1)));       // + v bb_1 - bb_1
-  }
-  CESS_MEMBAR();
-  {
-    const fp2 x = add(mul_nr(mul(add_nr(f.ld(2), f.ld(5)), e)), u0);
-    d.st(3, sub(add(sub(x, d.ld(0)), mul_nr(t.ld(2))), t.ld(0)));
-  }
-  CESS_MEMBAR();
-  {
-    const fp2 x = add(mul(add_nr(f.ld(2), f.ld(5)), c0), u1);
-    d.st(5, sub(add(sub(x, d.ld(2)), t.ld(1)), t.ld(2)));
-  }
-}
-
 // f <- f^2 for f in the cyclotomic subgroup (Granger-Scott, eprint 2009/565)
 template <class S>
 CESS_HD void cycsq12(const S& f) {
@@ -339,32 +277,17 @@ CESS_HD void inv12(const S& f) {
 // once in the code object; the hard part's five cyclotomic exponentiations by
 // x are spelled out as square runs and multiplies by the base.
 // ---------------------------------------------------------------------------
-enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_CHAIN, FE_END };
-enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6,
-                        SL_X0, SL_X1, SL_X2, SL_X3, SL_X4, SL_X5, SL_N };
+enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_END };
+enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6, SL_N };
 
-// a^x (x = -0xd201000000010000) for a in slot s.
-// Default: bits below the top one are 62, 60, 57, 48, 16 -> Granger-Scott
-// square runs 1, 2, 3, 9, 32, 16 interleaved with multiplies by the base.
-// CESS_FE_KARABINA=1: |x| has bits 63, 62, 60, 57, 48, 16, so a^|x| = a^(2^63)
-// a^(2^62) a^(2^60) a^(2^57) a^(2^48) a^(2^16); FE_CHAIN s runs the 63 squarings
-// in compressed form and leaves the six powers, decompressed with one
-// inversion, in slots X5..X0, and the multiplies follow.  Bit-exact (host
-// emulation and GPU tests), but measured slower on MI355X (k_final 222 ms vs
-// 208 ms per 1 M: 2.2 KB/lane of scratch in the register-resident compressed
-// loop), so it is off.
-#ifndef CESS_FE_KARABINA
-#define CESS_FE_KARABINA 0
-#endif
-#if CESS_FE_KARABINA
-#define CESS_FE_CYCEXP(s) \
-  {FE_CHAIN, s}, {FE_LOAD, SL_X5}, {FE_MUL, SL_X4}, {FE_MUL, SL_X3}, {FE_MUL, SL_X2}, {FE_MUL, SL_X1}, \
-      {FE_MUL, SL_X0}, {FE_CONJ, 0}
-#else
+// a^x (x = -0xd201000000010000) for a in slot s: |x| has bits 63, 62, 60, 57,
+// 48, 16, so the bits below the top one give Granger-Scott square runs of
+// 1, 2, 3, 9, 32, 16 interleaved with multiplies by the base.  (Karabina's
+// compressed squaring for these runs was measured slower on MI355X in round 1,
+// k_final 222 vs 208 ms per 1 M, and removed)
 #define CESS_FE_CYCEXP(s) \
   {FE_LOAD, s}, {FE_SQN, 1}, {FE_MUL, s}, {FE_SQN, 2}, {FE_MUL, s}, {FE_SQN, 3}, {FE_MUL, s}, {FE_SQN, 9}, \
       {FE_MUL, s}, {FE_SQN, 32}, {FE_MUL, s}, {FE_SQN, 16}, {FE_CONJ, 0}
-#endif
 
 // easy part: m = f^((p^6 - 1)(p^2 + 1)); hard part as in pairing.hpp
 // final_exponentiation (t2 = m).  SL_T0 doubles as scratch in the easy part.
@@ -433,77 +356,6 @@ CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
   acc.st(5, z5);
 }
 
-// FE_CHAIN: the powers a^(2^k), k = 16, 48, 57, 60, 62, 63, of the cyclotomic
-// element a (store `base`) into the stores X(0..5).  The 63 squarings run on
-// (z2, z3, z4, z5) in registers (cyc_sqr_compressed); z1 of the six powers is
-// recovered with ONE Fp2 inversion (Montgomery's simultaneous-inversion trick:
-// prefix products of the denominators parked in the z0 words, numerators in the
-// z1 words), then z0.  A lane whose denominator is zero (z2 = z3 = 0, e.g. a = 1
-// from an identity pair) recomputes its chain with full Granger-Scott squarings
-// (divergent, rare).  Costs 63 x 4 Fp2 products + ~0.25k multiplies, against
-// 63 x 9 Fp2 squarings.
-template <class B, class XFn, class P>
-CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
-  {
-    fp2 z2 = base.ld(3), z3 = base.ld(2), z4 = base.ld(1), z5 = base.ld(5);
-    int k = 0;
-#pragma unroll 1
-    for (int j = 0; j < 6; j++) {
-      const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
-#pragma unroll 1
-      for (; k < stop; k++) {
-        cyc_sqr_compressed(z2, z3, z4, z5);
-        CESS_MEMBAR();
-      }
-      const auto x = X(j);
-      x.st(3, z2);
-      x.st(2, z3);
-      x.st(1, z4);
-      x.st(5, z5);
-      CESS_MEMBAR();
-    }
-  }
-  bool degen = false;
-  fp2 prod = fp2_one();
-#pragma unroll 1
-  for (int j = 0; j < 6; j++) {
-    const auto x = X(j);
-    fp2 num, den;
-    cyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
-    const bool z = is_zero(den);
-    degen = degen || z;
-    x.st(4, num);
-    x.st(0, prod);   // product of the denominators before j
-    prod = mul(prod, select(z, fp2_one(), den));
-    CESS_MEMBAR();
-  }
-  fp2 iv = inv(prod);
-#pragma unroll 1
-  for (int j = 5; j >= 0; j--) {
-    const auto x = X(j);
-    fp2 num, den;
-    const fp2 z2 = x.ld(3), z3 = x.ld(2), z4 = x.ld(1), z5 = x.ld(5);
-    cyc_z1_frac(z2, z3, z4, z5, num, den);
-    const fp2 ivj = mul(iv, x.ld(0));   // 1 / den_j
-    iv = mul(iv, select(is_zero(den), fp2_one(), den));
-    const fp2 z1 = mul(x.ld(4), ivj);
-    x.st(4, z1);
-    x.st(0, cyc_z0(z1, z2, z3, z4, z5));
-    CESS_MEMBAR();
-  }
-  if (degen) {   // full squarings on X(5) as the running power
-    const auto w = X(5);
-    copy12(w, base);
-#pragma unroll 1
-    for (int j = 0; j < 5; j++) {
-      const int run = j == 0 ? 16 : j == 1 ? 32 : j == 2 ? 9 : j == 3 ? 3 : 2;
-      cyc_square_run_parked(w, pk, run);
-      copy12(X(j), w);
-    }
-    cyc_square_run_parked(w, pk, 1);
-  }
-}
-
 // Run the program.  The accumulator alternates between the stores acc0 and
 // acc1: FE_MUL writes the product of the current one and a slot into the other
 // (mul12_stream, with the parking store `pk` as its Fp6 temporary); every other
@@ -526,31 +378,10 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
         mul12_stream(cur ? acc0 : acc1, acc, slot(arg), pk);
         cur ^= 1;
         break;
-      case FE_SQN: {
-#if defined(CESS_FE_SQN_PARK)
-        cyc_square_run_parked(acc, pk, arg);
-#elif defined(CESS_FE_SQN_REGS)
-        // square run with the accumulator held in registers (one load/store per run)
-        fp12 t;
-        fp2* e = &t.c0.c0;
-#pragma unroll
-        for (int k = 0; k < 6; k++) e[k] = acc.ld(k);
-#pragma unroll 1
-        for (int r = 0; r < arg; r++) t = cyclotomic_square(t);
-#pragma unroll
-        for (int k = 0; k < 6; k++) acc.st(k, e[k]);
-#else
-#pragma unroll 1
-        for (int r = 0; r < arg; r++) cycsq12(acc);
-#endif
-        break;
-      }
+      case FE_SQN: cyc_square_run_parked(acc, pk, arg); break;
       case FE_CONJ: conj12(acc); break;
       case FE_FROB: frob12(acc, arg); break;
       case FE_INV: inv12(acc); break;
-#if CESS_FE_KARABINA
-      case FE_CHAIN: cyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }, pk); break;
-#endif
       default: break;
     }
   }
@@ -579,36 +410,6 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
     CESS_MEMBAR();
   }
   conj12(f);   // x < 0
-}
-
-// Miller loop with the accumulator ping-ponging between two stores fa, fb
-// (every Fp12 step reads one and writes the other) and one Fp6 temporary t;
-// otherwise as miller_loop2_staged.  Returns the index (0: fa, 1: fb) of the
-// store holding the result.
-template <class S, class T, class Pt, class Src>
-CESS_HD int miller_loop2_pp(const S& fa, const S& fb, const T& t, bool use0, bool use1, Pt&& pt, Src&& src) {
-  set_one12(fa);
-  int cur = 0;
-#pragma unroll 1
-  for (int s = 0; s < N_COEFFS; s++) {
-#pragma unroll 1
-    for (int pair = 0; pair < 2; pair++) {
-      if (!(pair ? use1 : use0)) continue;
-      coeff3 k = src(pair, s);
-      g1a p = pt(pair);
-      fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
-      mul014_stream(cur ? fa : fb, cur ? fb : fa, k.c2, c1, c4, t);
-      cur ^= 1;
-      CESS_MEMBAR();
-    }
-    if (square_after_step(s)) {
-      sqr12_stream(cur ? fa : fb, cur ? fb : fa, t);
-      cur ^= 1;
-    }
-    CESS_MEMBAR();
-  }
-  conj12(cur ? fb : fa);   // x < 0
-  return cur;
 }
 
 }  // namespace bls

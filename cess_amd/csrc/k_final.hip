@@ -7,7 +7,6 @@
 // Miller-loop output is slot SL_F.  Cyclotomic square runs hold the accumulator in
 // registers, with a third of it parked in LDS (two waves per SIMD).
 #include <hip/hip_runtime.h>
-#define CESS_FE_SQN_PARK 1
 #include "soa.hpp"
 
 using namespace bls;

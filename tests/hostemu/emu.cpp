@@ -2,7 +2,6 @@
 // (CESS_HOSTEMU) so tests can check the kernel algorithms against the oracle on
 // a machine without a GPU.  Never linked into the product library.
 #include <string.h>
-#define CESS_FE_SQN_PARK 1   // the square-run variant k_final uses
 #include "../../cess_amd/csrc/bls/h2c.hpp"
 #include "../../cess_amd/csrc/bls/staged.hpp"
 
@@ -138,12 +137,6 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   pts[1] = h;
   miller_loop2_staged(ArrF12{&slots[SL_F]}, !s.inf, !(q.inf || h.inf), [](int pair) { return pts[pair]; },
                       [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
-  // the ping-pong Miller loop (k_miller CESS_MILLER_MODE 3) must agree
-  static fp12 pa, pb, pt6;
-  const int w = miller_loop2_pp(ArrF12{&pa}, ArrF12{&pb}, ArrF12{&pt6}, !s.inf, !(q.inf || h.inf),
-                                [](int pair) { return pts[pair]; },
-                                [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
-  if (!eq(w ? pb : pa, slots[SL_F])) return 9;
   static fp12 park, acc1;
   const int which = final_exp_staged(ArrF12{&acc}, ArrF12{&acc1}, prog, [](int sl) { return ArrF12{&slots[sl]}; },
                                      ArrF12{&park});

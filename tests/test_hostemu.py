@@ -126,22 +126,3 @@ def test_cpu_baseline_path_codes(vectors):
     codes = (ctypes.c_uint8 * n)()
     cpu.cpu_verify_batch(ctypes.c_uint64(n), sigs, msgs, ctypes.c_uint32(32), pks, codes, ctypes.c_int(4))
     assert list(codes) == [c["code"] for c in cases]
-
-
-def test_karabina_chain_option(vectors):
-    """The optional compressed-squaring exponentiation (CESS_FE_KARABINA=1, off
-    by default: measured slower on MI355X) stays bit-exact: golden codes and Gt
-    bytes, including the identity pairs that take its uncompressed fallback."""
-    lib = os.path.join(HERE, "hostemu", "libemu_karabina.so")
-    hdr_dir = os.path.join(HERE, "..", "cess_amd", "csrc", "bls")
-    newest = max([os.path.getmtime(SRC)] + [os.path.getmtime(os.path.join(hdr_dir, f)) for f in os.listdir(hdr_dir)])
-    if not os.path.exists(lib) or os.path.getmtime(lib) < newest:
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-DCESS_HOSTEMU", "-DCESS_FE_KARABINA=1", "-shared", "-fPIC",
-                               SRC, "-o", lib])
-    emu = ctypes.CDLL(lib)
-    for c in vectors["cases"]:
-        s, m, k = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
-        gt = (ctypes.c_uint8 * 576)()
-        assert emu.emu_verify(s, m, len(m), k, gt) == c["code"], c["name"]
-        if "gt" in c:
-            assert bytes(gt).hex() == c["gt"], c["name"]

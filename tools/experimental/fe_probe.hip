@@ -11,7 +11,7 @@
 #include <vector>
 
 #include "soa.hpp"
-#include "bls/pair2.hpp"
+#include "pair2.hpp"   // tools/experimental (not a product header)
 
 using namespace bls;
 using namespace cess;

@@ -19,7 +19,7 @@
 // The single-lane versions in staged.hpp are the executable specification;
 // tools/fe_probe.hip and the GPU parity tests check these against them.
 #pragma once
-#include "staged.hpp"
+#include "bls/staged.hpp"
 
 #if !defined(CESS_HOSTEMU)
 namespace bls {

@@ -55,6 +55,16 @@ __device__ void rlc_scalar(const uint32_t* seed, uint64_t i, uint32_t (&k)[4]) {
 // computed every window and kept by a select (no divergent branches): 128
 // doublings + 64 complete additions (a per-bit ladder costs 128 + 128 here,
 // since some lane of the wave always takes the add).
+// Force-inlined on purpose.  Round 1 saw the out-of-line (__noinline__) form
+// hang; tools/rlc_call_probe.hip reproduces it and the ISA shows the cause: the
+// callee body is longer than s_branch's +-2^15-dword reach, so branch
+// relaxation expands long branches as s_getpc/s_add/s_setpc through s[30:31]
+// -- the return-address pair of the AMDGPU call ABI -- without saving it.  The
+// loop exit jumps to the return block through s[30:31] = &return block, and
+// the return's s_setpc_b64 s[30:31] then spins on itself forever.  A compiler
+// (branch-relaxation scavenging) defect, not a data race: the product library
+// therefore contains no device calls at all (tests/test_isa_guard.py checks
+// the shipped code objects for s_swappc_b64).
 __device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint32_t (&k)[4]) {
   const g1p T1 = {px, py, fp_one()};
   const g1p T2 = proj_dbl(T1);

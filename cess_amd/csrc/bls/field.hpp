@@ -43,15 +43,18 @@ namespace bls {
 #if defined(CESS_COUNT_OPS)
 // host test harness only: Fp multiply / square counters (algorithmic work)
 // (g_mul2_count: lazily reduced Fp2 products = 3 half-products + 2 reductions,
-// i.e. 2.5 Fp multiplies of work)
-inline uint64_t g_mul_count = 0, g_sqr_count = 0, g_mul2_count = 0;
+// i.e. 2.5 Fp multiplies of work; g_half_count: other lazily reduced forms in
+// half-multiply units, one per 196-mad half-product or reduction: dot2 = 8)
+inline uint64_t g_mul_count = 0, g_sqr_count = 0, g_mul2_count = 0, g_half_count = 0;
 #define CESS_COUNT_MUL() (++g_mul_count)
 #define CESS_COUNT_SQR() (++g_sqr_count)
 #define CESS_COUNT_MUL2() (++g_mul2_count)
+#define CESS_COUNT_HALVES(n) (g_half_count += (n))
 #else
 #define CESS_COUNT_MUL() ((void)0)
 #define CESS_COUNT_SQR() ((void)0)
 #define CESS_COUNT_MUL2() ((void)0)
+#define CESS_COUNT_HALVES(n) ((void)0)
 #endif
 
 struct fp {
@@ -242,6 +245,9 @@ CESS_HD uint64_t zero_after(uint64_t x) {
 // --- 28-bit compute domain ---------------------------------------------------
 constexpr uint32_t M28 = 0x0fffffffu;
 
+// acc += x * y (one v_mad_u64_u32; column sums stay below 2^64)
+CESS_HD void mac(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
+
 // 384-bit value (12 x 32) -> 14 x 28-bit limbs
 CESS_HD void unpack28(const fp& a, uint32_t (&l)[14]) {
 #pragma unroll
@@ -276,16 +282,16 @@ CESS_HD fp mont28(Col&& col) {
   for (int k = 0; k < 14; k++) {
     col(k, acc);
 #pragma unroll
-    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * c::P28[k - i];
+    for (int i = 0; i < k; i++) mac(acc, m[i], c::P28[k - i]);
     m[k] = ((uint32_t)acc * c::PINV28) & M28;
-    acc += (uint64_t)m[k] * c::P28[0];
+    mac(acc, m[k], c::P28[0]);
     acc >>= 28;
   }
 #pragma unroll
   for (int k = 14; k < 27; k++) {
     col(k, acc);
 #pragma unroll
-    for (int i = k - 13; i < 14; i++) acc += (uint64_t)m[i] * c::P28[k - i];
+    for (int i = k - 13; i < 14; i++) mac(acc, m[i], c::P28[k - i]);
     t[k - 14] = (uint32_t)acc & M28;
     acc >>= 28;
   }
@@ -304,13 +310,13 @@ CESS_HD void mont28x2(Col&& col, fp& out0, fp& out1) {
     col(k, acc0, acc1);
 #pragma unroll
     for (int i = 0; i < k; i++) {
-      acc0 += (uint64_t)m0[i] * c::P28[k - i];
-      acc1 += (uint64_t)m1[i] * c::P28[k - i];
+      mac(acc0, m0[i], c::P28[k - i]);
+      mac(acc1, m1[i], c::P28[k - i]);
     }
     m0[k] = ((uint32_t)acc0 * c::PINV28) & M28;
     m1[k] = ((uint32_t)acc1 * c::PINV28) & M28;
-    acc0 += (uint64_t)m0[k] * c::P28[0];
-    acc1 += (uint64_t)m1[k] * c::P28[0];
+    mac(acc0, m0[k], c::P28[0]);
+    mac(acc1, m1[k], c::P28[0]);
     acc0 >>= 28;
     acc1 >>= 28;
   }
@@ -319,8 +325,8 @@ CESS_HD void mont28x2(Col&& col, fp& out0, fp& out1) {
     col(k, acc0, acc1);
 #pragma unroll
     for (int i = k - 13; i < 14; i++) {
-      acc0 += (uint64_t)m0[i] * c::P28[k - i];
-      acc1 += (uint64_t)m1[i] * c::P28[k - i];
+      mac(acc0, m0[i], c::P28[k - i]);
+      mac(acc1, m1[i], c::P28[k - i]);
     }
     t0[k - 14] = (uint32_t)acc0 & M28;
     t1[k - 14] = (uint32_t)acc1 & M28;
@@ -345,7 +351,7 @@ CESS_HD fp mul(const fp& a0, const fp& b0) {
   fp r = mont28([&](int k, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++)
-      if (k - i >= 0 && k - i < 14) acc += (uint64_t)x[i] * y[k - i];
+      if (k - i >= 0 && k - i < 14) mac(acc, x[i], y[k - i]);
   });
   seq(r);
   return r;
@@ -364,9 +370,9 @@ CESS_HD fp sqr(const fp& a0) {
 #pragma unroll
     for (int i = 0; i < 14; i++) {
       const int j = k - i;
-      if (j > i && j < 14) acc += (uint64_t)x[i] * x2[j];
+      if (j > i && j < 14) mac(acc, x[i], x2[j]);
     }
-    if ((k & 1) == 0 && (k >> 1) < 14) acc += (uint64_t)x[k >> 1] * x[k >> 1];
+    if ((k & 1) == 0 && (k >> 1) < 14) mac(acc, x[k >> 1], x[k >> 1]);
   });
   seq(r);
   return r;
@@ -582,9 +588,9 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
           if (j < 0 || j >= 14) continue;
-          v0 += (uint64_t)x0[i] * y0[j];
-          v1 += (uint64_t)x1[i] * y1[j];
-          acc1 += (uint64_t)xs[i] * ys[j];
+          mac(v0, x0[i], y0[j]);
+          mac(v1, x1[i], y1[j]);
+          mac(acc1, xs[i], ys[j]);
         }
         acc0 += v0 + c::LAZY_M28[k];
         acc0 -= v1;
@@ -596,6 +602,66 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   return r;
 }
 #endif
+// a*b + c*d over Fp2 with ONE Montgomery reduction per output component: the
+// two Karatsuba products are accumulated column by column into the same three
+// sums (v0, v1, t) before the lazy combination of mul(fp2, fp2) above, so the
+// pair costs 6 half-products + 2 reductions (1,568 mads) instead of two full
+// products (1,960) and an Fp2 addition.  Same input contract as mul(fp2, fp2)
+// (components < 2^384, e.g. add_nr sums).  Bounds: columns of t stay below
+// 2 x 14 x 2^58 + 14 x 2^56 < 2^63.1; c0 = v0 - v1 + 2 M < 2^771 and
+// c1 = t - v0 - v1 < 2^771, both below p R = 2^772.7, so each reduction
+// returns < 2p.
+CESS_HD fp2 dot2(const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
+  CESS_COUNT_HALVES(8);
+  fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1, c0 = c.c0, c1 = c.c1, d0 = d.c0, d1 = d.c1;
+  seq(a0);
+  seq(a1);
+  seq(b0);
+  seq(b1);
+  seq(c0);
+  seq(c1);
+  seq(d0);
+  seq(d1);
+  uint32_t xa0[14], xa1[14], yb0[14], yb1[14], xc0[14], xc1[14], yd0[14], yd1[14];
+  uint32_t xas[14], ybs[14], xcs[14], yds[14];
+  unpack28(a0, xa0);
+  unpack28(a1, xa1);
+  unpack28(b0, yb0);
+  unpack28(b1, yb1);
+  unpack28(c0, xc0);
+  unpack28(c1, xc1);
+  unpack28(d0, yd0);
+  unpack28(d1, yd1);
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    xas[i] = xa0[i] + xa1[i], ybs[i] = yb0[i] + yb1[i];
+    xcs[i] = xc0[i] + xc1[i], yds[i] = yd0[i] + yd1[i];
+  }
+  fp2 r;
+  mont28x2(
+      [&](int k, uint64_t& acc0, uint64_t& acc1) {
+        uint64_t v0 = zero_after(acc1), v1 = zero_after(acc0);
+#pragma unroll
+        for (int i = 0; i < 14; i++) {
+          const int j = k - i;
+          if (j < 0 || j >= 14) continue;
+          mac(v0, xa0[i], yb0[j]);
+          mac(v1, xa1[i], yb1[j]);
+          mac(acc1, xas[i], ybs[j]);
+          mac(v0, xc0[i], yd0[j]);
+          mac(v1, xc1[i], yd1[j]);
+          mac(acc1, xcs[i], yds[j]);
+        }
+        acc0 += v0 + 2 * c::LAZY_M28[k];
+        acc0 -= v1;
+        acc1 -= v0 + v1;
+      },
+      r.c0, r.c1);
+  seq(r.c0);
+  seq(r.c1);
+  return r;
+}
+
 CESS_HD fp2 sqr(const fp2& a) {   // a must be reduced (sub below)
   fp t0 = mul(add_nr(a.c0, a.c1), sub(a.c0, a.c1));
   fp t1 = mul(a.c0, a.c1);
@@ -768,6 +834,11 @@ CESS_HD fp12 frobenius(const fp12& a) {
 }
 
 // Granger-Scott squaring in the cyclotomic subgroup (eprint 2009/565)
+// (a + b s)^2 in Fp4 = Fp2[s]/(s^2 - xi): c0 = a^2 + xi b^2, c1 = 2ab.
+// (A single-reduction form of c0 -- five half-products accumulated with
+// digit-negated operands, two reductions -- issues 8 % fewer instructions in
+// the square run but needs ~190 registers and spills at two waves per SIMD:
+// k_final 221.7 vs 211.9 ms per 1 M, profiles/r02g_sweep.txt.)
 CESS_HD void fp4_square(fp2& c0, fp2& c1, const fp2& a, const fp2& b) {
   fp2 t0 = sqr(a);
   fp2 t1 = sqr(b);

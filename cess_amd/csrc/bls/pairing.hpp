@@ -80,6 +80,19 @@ CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink) {
   sink(idx++, doubling_step(r));
 }
 
+// Scale a line by 1/c2: (c0, c1, c2) -> (c0/c2, c1/c2, 1).  Every Fp2 factor of
+// the Miller-loop value dies in the final exponentiation ((p^2 - 1) divides
+// (p^12 - 1)/r), so the Gt value is unchanged, and the sparse product with a
+// line whose c2 is one costs 9 Fp2 products instead of 13 (staged.hpp
+// mul014_one).  Used for the constant -G2 table (G2PREPARED_NEG_G, A10), built
+// once per context.
+CESS_HD void normalize_line(coeff3& k) {
+  const fp2 ic2 = inv(k.c2);
+  k.c0 = mul(k.c0, ic2);
+  k.c1 = mul(k.c1, ic2);
+  k.c2 = fp2_one();
+}
+
 CESS_HD fp12 ell(const fp12& f, const coeff3& k, const fp& px, const fp& py) {
   return mul_by_014(f, k.c2, mul_fp(k.c1, px), mul_fp(k.c0, py));
 }

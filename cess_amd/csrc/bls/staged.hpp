@@ -146,12 +146,29 @@ CESS_HD void sqr12(const S& f) {
   st6(f, 1, dbl(ab));
 }
 
+// a * (b0 + b1 v) for an Fp6 `a` in store half h (coefficients fetched per
+// use): each output coefficient is a sum of two Fp2 products, taken as one
+// dot2 (one reduction per component): (a0 b0 + a2 (xi b1), a0 b1 + a1 b0,
+// a1 b1 + a2 b0) -- 3 x 1,568 mads against mul_by_01's 5 x 980 plus the
+// reductions and additions of its Karatsuba recombination (k_miller 179.6 vs
+// 184.4 ms per 1 M, profiles/r02g_sweep.txt).  xb1 = xi * b1.
+template <class S>
+CESS_HD fp6 mul_by_01_dot(const S& f, int h, const fp2& b0, const fp2& b1, const fp2& xb1) {
+  fp6 r;
+  r.c0 = dot2(f.ld(3 * h), b0, f.ld(3 * h + 2), xb1);
+  CESS_MEMBAR();
+  r.c1 = dot2(f.ld(3 * h), b1, f.ld(3 * h + 1), b0);
+  CESS_MEMBAR();
+  r.c2 = dot2(f.ld(3 * h + 1), b1, f.ld(3 * h + 2), b0);
+  return r;
+}
+
 // f <- f * (c0 + c1 v + c4 v w)   (bls12_381 Fp12::mul_by_014, in place)
 template <class S>
 CESS_HD void mul014(const S& f, const fp2& c0, const fp2& c1, const fp2& c4) {
   fp6 bb = mul_by_1(ld6(f, 1), c4);
   CESS_MEMBAR();
-  fp6 aa = mul_by_01(ld6(f, 0), c0, c1);
+  fp6 aa = mul_by_01_dot(f, 0, c0, c1, mul_nr(c1));
   CESS_MEMBAR();
   {
     fp6 s = add(ld6(f, 0), ld6(f, 1));
@@ -160,7 +177,32 @@ CESS_HD void mul014(const S& f, const fp2& c0, const fp2& c1, const fp2& c4) {
   st6(f, 0, add(mul_v(bb), aa));
   fp6 u = add(aa, bb);
   CESS_MEMBAR();
-  fp6 t = mul_by_01(ld6(f, 1), c0, add_nr(c1, c4));
+  const fp2 d = add(c1, c4);
+  fp6 t = mul_by_01_dot(f, 1, c0, d, mul_nr(d));
+  st6(f, 1, sub(t, u));
+}
+
+// a * (1 + b1 v): mul_by_01 with b0 = 1 (a reduced)
+CESS_HD fp6 mul_by_01_one(const fp6& a, const fp2& b1) {
+  return {add(a.c0, mul_nr(mul(a.c2, b1))), add(a.c1, mul(a.c0, b1)), add(a.c2, mul(a.c1, b1))};
+}
+
+// f <- f * (1 + c1 v + c4 v w): mul014 for a line normalised to c0 = 1
+// (pairing.hpp normalize_line), 9 Fp2 products instead of 13
+template <class S>
+CESS_HD void mul014_one(const S& f, const fp2& c1, const fp2& c4) {
+  fp6 bb = mul_by_1(ld6(f, 1), c4);
+  CESS_MEMBAR();
+  fp6 aa = mul_by_01_one(ld6(f, 0), c1);
+  CESS_MEMBAR();
+  {
+    fp6 s = add(ld6(f, 0), ld6(f, 1));
+    st6(f, 1, s);                    // f.c1 <- a0 + a1 (consumed below)
+  }
+  st6(f, 0, add(mul_v(bb), aa));
+  fp6 u = add(aa, bb);
+  CESS_MEMBAR();
+  fp6 t = mul_by_01_one(ld6(f, 1), add(c1, c4));
   st6(f, 1, sub(t, u));
 }
 
@@ -283,8 +325,9 @@ enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6
 // a^x (x = -0xd201000000010000) for a in slot s: |x| has bits 63, 62, 60, 57,
 // 48, 16, so the bits below the top one give Granger-Scott square runs of
 // 1, 2, 3, 9, 32, 16 interleaved with multiplies by the base.  (Karabina's
-// compressed squaring for these runs was measured slower on MI355X in round 1,
-// k_final 222 vs 208 ms per 1 M, and removed)
+// compressed squaring saves a third of the products of a run, but each of the
+// five exponentiations then needs one Fp2 inversion to decompress its six
+// powers, ~460 multiplies: no net gain -- DESIGN.md §5.)
 #define CESS_FE_CYCEXP(s) \
   {FE_LOAD, s}, {FE_SQN, 1}, {FE_MUL, s}, {FE_SQN, 2}, {FE_MUL, s}, {FE_SQN, 3}, {FE_MUL, s}, {FE_SQN, 9}, \
       {FE_MUL, s}, {FE_SQN, 32}, {FE_MUL, s}, {FE_SQN, 16}, {FE_CONJ, 0}
@@ -389,7 +432,8 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
 }
 
 // Miller loop for the two pairs of PublicKey::verify on an accumulator store:
-// pair 0 = (sig, -G2) (uniform -G2 table), pair 1 = (H(m), pk).  use0/use1:
+// pair 0 = (sig, -G2) (uniform -G2 table, lines normalised to c2 = 1 by
+// normalize_line), pair 1 = (H(m), pk).  use0/use1:
 // the pair's points are both non-identity (identity terms contribute 1).
 // pt(pair) yields the pair's affine G1 point; src(pair, step) its coefficients.
 template <class S, class Pt, class Src>
@@ -403,7 +447,10 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
       coeff3 k = src(pair, s);
       g1a p = pt(pair);
       fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
-      mul014(f, k.c2, c1, c4);
+      if (pair)
+        mul014(f, k.c2, c1, c4);
+      else
+        mul014_one(f, c1, c4);   // -G2 table: lines normalised to c2 = 1
       CESS_MEMBAR();
     }
     if (square_after_step(s)) sqr12(f);

@@ -168,6 +168,7 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
   }
   hipLaunchKernelGGL(k_prepare, dim3(1), dim3(64), 0, c->stream, (uint64_t)1, tmp.as<uint32_t>(), c->neg_g2.as<uint4>(),
                      (uint64_t)1);
+  hipLaunchKernelGGL(k_norm_lines, dim3(1), dim3(128), 0, c->stream, c->neg_g2.as<uint4>());
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     cess_bls_ctx_destroy(c);
     return CESS_BLS_E_HIP;

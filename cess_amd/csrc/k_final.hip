@@ -14,6 +14,8 @@ using namespace cess;
 
 __constant__ uint8_t kFeProgram[][2] = {CESS_FE_PROGRAM};
 
+// two waves per SIMD (one wave with 512 registers and no scratch measured
+// slower: 245 vs 212 ms per 1 M, profiles/r02g_sweep.txt)
 #define CESS_LB_F12 __launch_bounds__(256, 2)
 
 __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,

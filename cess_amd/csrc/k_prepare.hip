@@ -17,3 +17,13 @@ __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_af
   fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
   g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); });
 }
+
+// The constant -G2 table (one lane per line, stride 1): scale every line to
+// c2 = 1 (pairing.hpp normalize_line), once per context after k_prepare built it.
+__global__ __launch_bounds__(128) void k_norm_lines(uint4* __restrict__ tab) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N_COEFFS) return;
+  coeff3 c = ld_coeff4(tab, 1, 0, k);
+  normalize_line(c);
+  st_coeff4(tab, 1, 0, k, c);
+}

@@ -76,6 +76,7 @@ static void init_neg_g2() {
   fp2 gx = {fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)};
   fp2 gy = neg(fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)});
   g2_prepare(gx, gy, [](int i, const coeff3& k) { g_neg_g2[i] = k; });
+  for (int i = 0; i < N_COEFFS; i++) normalize_line(g_neg_g2[i]);   // as the device table (k_norm_lines)
   g_init = true;
 }
 
@@ -88,11 +89,11 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
   be_words(sig, 12, ws);
   be_words(pk, 24, wp);
   auto snap = [&](int st) {
-    out[2 * st] = 2 * g_mul_count + 5 * g_mul2_count;   // half-multiplies
+    out[2 * st] = 2 * g_mul_count + 5 * g_mul2_count + g_half_count;   // half-multiplies
     out[2 * st + 1] = g_sqr_count;
-    g_mul_count = g_sqr_count = g_mul2_count = 0;
+    g_mul_count = g_sqr_count = g_mul2_count = g_half_count = 0;
   };
-  g_mul_count = g_sqr_count = g_mul2_count = 0;
+  g_mul_count = g_sqr_count = g_mul2_count = g_half_count = 0;
   g1a s;
   g1_decompress(ws, s);
   snap(0);
@@ -104,10 +105,17 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
   static coeff3 pkc[N_COEFFS];
   g2_prepare(q.x, q.y, [](int i, const coeff3& k) { pkc[i] = k; });
   snap(3);
-  fp12 f = miller_loop2(s, false, h, false, [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+  // the staged Miller loop and final-exponentiation program the kernels run
+  static fp12 slots[SL_N], acc, acc1, park;
+  static const uint8_t prog[][2] = {CESS_FE_PROGRAM};
+  static g1a pts[2];
+  pts[0] = s;
+  pts[1] = h;
+  miller_loop2_staged(ArrF12{&slots[SL_F]}, !s.inf, !(q.inf || h.inf), [](int pair) { return pts[pair]; },
+                      [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
   snap(4);
-  fp12 g = final_exponentiation(f);
-  (void)g;
+  (void)final_exp_staged(ArrF12{&acc}, ArrF12{&acc1}, prog, [](int sl) { return ArrF12{&slots[sl]}; },
+                         ArrF12{&park});
   snap(5);
 }
 #endif

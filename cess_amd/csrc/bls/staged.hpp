@@ -353,20 +353,23 @@ enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6
       /* t3 = frob2(t3 * t0) * t1 * t6 * t4 */ {FE_LOAD, SL_T3}, {FE_MUL, SL_T0}, {FE_FROB, 2}, {FE_MUL, SL_T1},  \
       {FE_MUL, SL_T6}, {FE_MUL, SL_T4}, {FE_END, 0}
 
-// n cyclotomic squarings of acc with z2..z5 in registers and z0, z1 (plus one
-// Fp2 temporary) parked in a 3-Fp2 store `pk` (LDS in k_final): the register
-// working set drops by 72 dwords, which is what the two-waves-per-SIMD budget
-// (256 VGPRs) lacks for the value-based run (measured: 270 -> 119 scratch
-// accesses per squaring).  Same formulas as cyclotomic_square (field.hpp):
-// pair (z0, z1) updates itself; the square of (z2, z3) updates z4, z5 and the
-// square of (z4, z5) updates z2, z3, so the latter is taken first and its t3
-// parked while the former runs.
+// n cyclotomic squarings of acc (Granger-Scott formulas, as cyclotomic_square
+// in field.hpp): pair (z0, z1) updates itself; the square of (z2, z3) updates
+// z4, z5 and the square of (z4, z5) updates z2, z3, so the latter is taken
+// first and its t3 parked while the former runs.  z0, z1 and that temporary
+// are parked in the 3-Fp2 store `pk` (LDS in k_final), z4, z5 stay in the
+// accumulator store `acc` (HBM in k_final) for the whole run, and only z2, z3
+// live in registers: the register peak is one Fp4 square's working set plus
+// three Fp2, which the two-waves-per-SIMD budget (256 VGPRs) nearly holds
+// (57 scratch accesses per squaring, against 101 with z2..z5 in registers;
+// same time, profiles/r02j_sweep.txt), for 4 Fp2 loads + 2 Fp2 stores of
+// `acc` per squaring.
 // store index: z0 = 0, z4 = 1, z3 = 2, z2 = 3, z1 = 4, z5 = 5
 template <class A, class P>
-CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
+CESS_HD void cyc_square_run(const A& acc, const P& pk, int n) {
   pk.st(0, acc.ld(0));
   pk.st(1, acc.ld(4));
-  fp2 z2 = acc.ld(3), z3 = acc.ld(2), z4 = acc.ld(1), z5 = acc.ld(5);
+  fp2 z2 = acc.ld(3), z3 = acc.ld(2);
 #pragma unroll 1
   for (int r = 0; r < n; r++) {
     CESS_MEMBAR();
@@ -378,14 +381,20 @@ CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
       pk.st(1, add(dbl(add(t1, b)), t1));
     }
     CESS_MEMBAR();
-    fp2 u0, u1;
-    fp4_square(u0, u1, z4, z5);
-    pk.st(2, u1);
+    fp2 u0;
+    {
+      fp2 u1;
+      fp4_square(u0, u1, acc.ld(1), acc.ld(5));   // (z4, z5)
+      pk.st(2, u1);
+    }
     CESS_MEMBAR();
-    fp2 t0, t1;
-    fp4_square(t0, t1, z2, z3);
-    z4 = add(dbl(sub(t0, z4)), t0);
-    z5 = add(dbl(add(t1, z5)), t1);
+    {
+      fp2 t0, t1;
+      fp4_square(t0, t1, z2, z3);
+      acc.st(1, add(dbl(sub(t0, acc.ld(1))), t0));   // z4
+      acc.st(5, add(dbl(add(t1, acc.ld(5))), t1));   // z5
+    }
+    CESS_MEMBAR();
     const fp2 n3 = mul_nr(pk.ld(2));
     z2 = add(dbl(add(n3, z2)), n3);
     z3 = add(dbl(sub(u0, z3)), u0);
@@ -395,8 +404,6 @@ CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
   acc.st(4, pk.ld(1));
   acc.st(3, z2);
   acc.st(2, z3);
-  acc.st(1, z4);
-  acc.st(5, z5);
 }
 
 // Run the program.  The accumulator alternates between the stores acc0 and
@@ -404,7 +411,7 @@ CESS_HD void cyc_square_run_parked(const A& acc, const P& pk, int n) {
 // (mul12_stream, with the parking store `pk` as its Fp6 temporary); every other
 // opcode works in place.  slot(s) returns the store of slot s (slot SL_F holds
 // the Miller-loop output on entry); `pk` is also the parking store of
-// cyc_square_run_parked.  Returns the index (0/1) of the store holding the
+// cyc_square_run.  Returns the index (0/1) of the store holding the
 // result.
 template <class A, class SlotFn, class P>
 CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)[2], SlotFn&& slot, const P& pk) {
@@ -421,7 +428,7 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
         mul12_stream(cur ? acc0 : acc1, acc, slot(arg), pk);
         cur ^= 1;
         break;
-      case FE_SQN: cyc_square_run_parked(acc, pk, arg); break;
+      case FE_SQN: cyc_square_run(acc, pk, arg); break;
       case FE_CONJ: conj12(acc); break;
       case FE_FROB: frob12(acc, arg); break;
       case FE_INV: inv12(acc); break;

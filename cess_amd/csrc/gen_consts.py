@@ -226,6 +226,15 @@ def main():
     M = sum(b << (28 * k) for k, b in enumerate(B))
     assert M % P == 0 and M < (1 << 770) and max(B) < (1 << 60)
     w("CESS_CONST uint64_t LAZY_M28[27] = {" + ", ".join(f"0x{x:016x}ull" for x in B) + "};")
+    # digit-wise negation: K - x with K = 0 mod p and every 28-bit digit of K at
+    # least the largest digit of a value < 2^384 (2^28 - 1, top digit 2^20 - 1),
+    # so K - x has non-negative digits (< 2^29) and represents -x mod p
+    base = [(1 << 28) - 1] * 13 + [(1 << 20) - 1]
+    bv = sum(b << (28 * k) for k, b in enumerate(base))
+    adj = (-bv) % P
+    K = [base[k] + ((adj >> (28 * k)) & ((1 << 28) - 1)) for k in range(14)]
+    assert sum(k << (28 * i) for i, k in enumerate(K)) % P == 0 and max(K) < (1 << 29)
+    w("CESS_CONST uint32_t NEG_K28[14] = {" + ", ".join(f"0x{x:08x}u" for x in K) + "};")
     arr("HALF", mont((P + 1) // 2))
     arr("P_HALF_RAW", (P - 1) // 2)
     # exponents (raw integers, little-endian words)

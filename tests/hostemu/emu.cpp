@@ -26,6 +26,22 @@ void emu_fp2_mul_mont(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0
   memcpy(out0, c0.v, 48);
   memcpy(out1, c1.v, 48);
 }
+// lazily reduced Fp2 square and dot2 on raw (possibly unreduced, < 2^384) limbs
+void emu_fp2_sqr_mont(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {
+  fp2 r = sqr(fp2{load_raw(a0), load_raw(a1)});
+  const fp c0 = fp_reduce_once(r.c0), c1 = fp_reduce_once(r.c1);
+  memcpy(out0, c0.v, 48);
+  memcpy(out1, c1.v, 48);
+}
+// in: 8 x 12 limbs (a0 a1 b0 b1 c0 c1 d0 d1); out: a*b + c*d (canonical)
+void emu_fp2_dot2_mont(const uint32_t* in, uint32_t* out0, uint32_t* out1) {
+  fp2 v[4];
+  for (int i = 0; i < 4; i++) v[i] = {load_raw(in + 24 * i), load_raw(in + 24 * i + 12)};
+  fp2 r = dot2(v[0], v[1], v[2], v[3]);
+  const fp c0 = fp_reduce_once(r.c0), c1 = fp_reduce_once(r.c1);
+  memcpy(out0, c0.v, 48);
+  memcpy(out1, c1.v, 48);
+}
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
 int emu_fp2_sqrt(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {
   fp2 a = {to_mont(load_raw(a0)), to_mont(load_raw(a1))}, r;

@@ -106,6 +106,37 @@ def test_fp2_mul_lazy_bounds(emu):
         assert val(r1) == (a0 * b1 + a1 * b0) * RINV % P, (a0, a1, b0, b1)
 
 
+def test_fp2_sqr_and_dot2_lazy_bounds(emu):
+    """The lazily reduced Fp2 square (one unpack, digit-negated a1 = K - a1)
+    and dot2 (a*b + c*d, one reduction per component) at the extremes of their
+    input contract -- components up to 2^384 - 1, 0, p, multiples of p -- and
+    random values; outputs must be the exact Montgomery products mod p."""
+    import random
+
+    import oracle.bls_oracle as o
+    P, RINV = o.P, pow(2, -392, o.P)
+    rng = random.Random(11)
+    limbs = lambda v: (ctypes.c_uint32 * 12)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+    val = lambda arr: sum(arr[i] << (32 * i) for i in range(12))
+    top = (1 << 384) - 1
+    edge = [0, 1, P - 1, P, 2 * P - 1, 4 * P - 1, 8 * P - 1, top, top - 1, 1 << 383, (1 << 364) - 1]
+    pick = lambda: rng.choice(edge) if rng.random() < 0.6 else rng.randrange(1 << 384)
+    for _ in range(300):
+        a0, a1 = pick(), pick()
+        r0, r1 = (ctypes.c_uint32 * 12)(), (ctypes.c_uint32 * 12)()
+        emu.emu_fp2_sqr_mont(limbs(a0), limbs(a1), r0, r1)
+        assert val(r0) == (a0 * a0 - a1 * a1) * RINV % P, (a0, a1)
+        assert val(r1) == (2 * a0 * a1) * RINV % P, (a0, a1)
+    for _ in range(300):
+        x = [pick() for _ in range(8)]
+        buf = (ctypes.c_uint32 * 96)(*[(v >> (32 * i)) & 0xFFFFFFFF for v in x for i in range(12)])
+        r0, r1 = (ctypes.c_uint32 * 12)(), (ctypes.c_uint32 * 12)()
+        emu.emu_fp2_dot2_mont(buf, r0, r1)
+        a0, a1, b0, b1, c0, c1, d0, d1 = x
+        assert val(r0) == (a0 * b0 - a1 * b1 + c0 * d0 - c1 * d1) * RINV % P, x
+        assert val(r1) == (a0 * b1 + a1 * b0 + c0 * d1 + c1 * d0) * RINV % P, x
+
+
 def test_cpu_baseline_path_codes(vectors):
     """bench.py's cpu_baseline leg (tests/hostemu/cpu_verify.cpp, multi-threaded)
     gives the golden verdict codes for every fixed-size case."""

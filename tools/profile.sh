@@ -8,6 +8,7 @@ TAG=${1:-r01}
 N=${2:-1048576}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+sha256sum cess_amd/lib/libcess_bls.so > $OUT/lib_sha256.txt
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 BENCH="python3 bench.py --n $N --steps 2 --warmup 1 --cpu-sample 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail -20 $OUT/trace.log; exit 1; }

@@ -20,16 +20,31 @@ dst = os.path.join(root, "profiles")
 stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
 if stats:
     shutil.copy(stats[0], os.path.join(dst, f"{tag}_rocprof_kernel_stats.csv"))
+# Per-dispatch attribution: a kernel's counters come from its dispatches over
+# the whole batch (grid = n) only -- e.g. the 64-thread k_prepare dispatch that
+# builds the -G2 table at context creation is excluded.  Counter values of one
+# dispatch are summed over its rows (XCD / SE instances).
 agg = {}
 for f in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
+        if int(r["Grid_Size"]) != n:
+            continue
         k = r["Kernel_Name"].split("(")[0]
         d = agg.setdefault(k, {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
                                "agpr": int(r.get("Accum_VGPR_Count", 0) or 0),
-                               "scratch_per_lane": int(r["Scratch_Size"]), "lds": int(r["LDS_Block_Size"])})
+                               "scratch_per_lane": int(r["Scratch_Size"]), "lds": int(r["LDS_Block_Size"]),
+                               "_dispatches": {}})
+        cnt = d["_dispatches"].setdefault(r["Counter_Name"], set())
+        cnt.add(r["Dispatch_Id"])
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-out = {"n": n, "source": f"profiles/{tag}_pmc_summary.txt", "all": {}}
-lines = [f"# rocprofv3 PMC summary, tag {tag} (bench.py --n {n} --steps 1 --warmup 0; one launch per kernel)",
+for d in agg.values():   # per launch: divide by the number of full-batch dispatches of that counter's pass
+    for c, ids in d.pop("_dispatches").items():
+        d[c] /= len(ids)
+sha_file = os.path.join(src, "lib_sha256.txt")
+lib_sha = open(sha_file).read().split()[0] if os.path.exists(sha_file) else None
+out = {"n": n, "source": f"profiles/{tag}_pmc_summary.txt", "lib_sha256": lib_sha, "all": {}}
+lines = [f"# rocprofv3 PMC summary, tag {tag} (bench.py --n {n} --steps 1 --warmup 0; per full-batch launch; "
+         f"libcess_bls.so sha256 {lib_sha})",
          "# separate passes: FETCH_SIZE | WRITE_SIZE | SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE",
          "# HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024  (FETCH_SIZE in KiB; gfx950 FETCH_SIZE reports 1/2 of wide reads)"]
 for k, d in sorted(agg.items()):

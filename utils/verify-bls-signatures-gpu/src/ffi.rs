@@ -119,4 +119,20 @@ extern "C" {
                                 reset: c_int) -> c_int;
     pub fn cess_bls_status_string(status: c_int) -> *const c_char;
     pub fn cess_bls_version() -> *const c_char;
+
+    // include/cess_rsa.h: cp_enclave_verify::verify_rsa (primitives/enclave-verify/src/lib.rs:221-228)
+    pub fn cess_rsa_parse_key(der: *const u8, len: usize, format: c_int, n_out: *mut u8, n_cap: usize,
+                              n_len: *mut usize, e_out: *mut u64) -> c_int;
+    pub fn cess_rsa_keys_load(ctx: *mut cess_bls_ctx, k: usize, ders: *const u8, der_offsets: *const u64,
+                              format: c_int, key_status_out: *mut c_int) -> c_int;
+    pub fn cess_rsa_verify_batch(ctx: *mut cess_bls_ctx, n: usize, key_idx: *const u32, sigs: *const u8,
+                                 sig_offsets: *const u64, msgs: *const u8, msg_offsets: *const u64,
+                                 codes_out: *mut u8, bitmap_out: *mut u64) -> c_int;
+    pub fn cess_rsa_verify(ctx: *mut cess_bls_ctx, key_der: *const u8, key_len: usize, msg: *const u8,
+                           msg_len: usize, sig: *const u8, sig_len: usize, ok_out: *mut c_int) -> c_int;
 }
+
+pub const CESS_RSA_E_UNSUPPORTED: c_int = -10;
+pub const CESS_RSA_KEY_SPKI: c_int = 0;
+pub const CESS_RSA_KEY_PKCS1: c_int = 1;
+pub const RSA_CODE_OK: u8 = 0;

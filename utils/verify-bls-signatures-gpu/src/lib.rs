@@ -263,6 +263,50 @@ impl Verifier {
         Ok(ok != 0)
     }
 
+    // --- RSA PKCS#1 v1.5 raw (include/cess_rsa.h) ------------------------------
+    /// `cp_enclave_verify::verify_rsa(key, msg, sig)` (primitives/enclave-verify/
+    /// src/lib.rs:221-228) without the panic: `Err(Error::BadKey)` where
+    /// `from_public_key_der(key).unwrap()` would panic.
+    pub fn verify_rsa(&mut self, key_der: &[u8], msg: &[u8], sig: &[u8]) -> Result<bool, Error> {
+        let mut ok: c_int = 0;
+        check(unsafe {
+            ffi::cess_rsa_verify(self.ctx, key_der.as_ptr(), key_der.len(), msg.as_ptr(), msg.len(), sig.as_ptr(),
+                                 sig.len(), &mut ok)
+        })?;
+        Ok(ok != 0)
+    }
+
+    /// Load a distinct-key table of DER keys (`format`: ffi::CESS_RSA_KEY_SPKI or
+    /// ffi::CESS_RSA_KEY_PKCS1, the latter for Podr2Key = [u8; 270]); returns
+    /// the per-key load status.
+    pub fn rsa_keys_load(&mut self, ders: &[&[u8]], format: i32) -> Result<Vec<i32>, Error> {
+        let mut data = Vec::new();
+        let o = offsets(ders.iter().copied(), &mut data);
+        let mut st = vec![0 as c_int; ders.len()];
+        check(unsafe {
+            ffi::cess_rsa_keys_load(self.ctx, ders.len(), data.as_ptr(), o.as_ptr(), format as c_int, st.as_mut_ptr())
+        })?;
+        Ok(st.into_iter().map(|x| x as i32).collect())
+    }
+
+    /// verify_rsa over a batch against the loaded key table: record i =
+    /// (key key_idx[i], msgs[i], sigs[i]); codes 0 OK, 1 SIG_LEN, 2 SIG_RANGE,
+    /// 3 MSG_LEN, 4 MISMATCH, 5 KEY (codes 1..5 are the reference's `false`).
+    pub fn verify_rsa_batch(&mut self, key_idx: &[u32], msgs: &[&[u8]], sigs: &[&[u8]]) -> Result<Verdicts, Error> {
+        assert!(key_idx.len() == msgs.len() && msgs.len() == sigs.len());
+        let n = key_idx.len();
+        let (mut md, mut sd) = (Vec::new(), Vec::new());
+        let mo = offsets(msgs.iter().copied(), &mut md);
+        let so = offsets(sigs.iter().copied(), &mut sd);
+        let mut codes = vec![0u8; n];
+        let mut bitmap = vec![0u64; (n + 63) / 64];
+        check(unsafe {
+            ffi::cess_rsa_verify_batch(self.ctx, n, key_idx.as_ptr(), sd.as_ptr(), so.as_ptr(), md.as_ptr(),
+                                       mo.as_ptr(), codes.as_mut_ptr(), bitmap.as_mut_ptr())
+        })?;
+        Ok(Verdicts { bitmap, codes })
+    }
+
     // --- generators (PrivateKey::public_key / sign, src/lib.rs:226-236) -------
     pub fn public_keys(&mut self, sks: &[[u8; 32]]) -> Result<Vec<[u8; 96]>, Error> {
         let flat: Vec<u8> = sks.iter().flat_map(|k| k.iter().copied()).collect();
@@ -479,6 +523,16 @@ pub fn verify_bls(key: &[u8], msg: &[u8], sig: &[u8]) -> Result<(), ()> {
         Err(Error::BadKey) => panic!("called `Result::unwrap()` on an `Err` value: {:?}", InvalidPublicKey::InvalidPoint),
         Err(Error::BadSig) => panic!("called `Result::unwrap()` on an `Err` value: {:?}", InvalidSignature::InvalidPoint),
         Err(e) => panic!("MI355X verifier: {}", e.message()),
+    }
+}
+
+/// `cp_enclave_verify::verify_rsa(key, msg, sig)` (primitives/enclave-verify/
+/// src/lib.rs:221-228) with the reference's semantics: panics if the key does
+/// not parse as SubjectPublicKeyInfo DER.
+pub fn verify_rsa(key: &[u8], msg: &[u8], sig: &[u8]) -> bool {
+    match with_default(|v| v.verify_rsa(key, msg, sig)) {
+        Ok(ok) => ok,
+        Err(e) => panic!("called `Result::unwrap()` on an `Err` value: {}", e.message()),
     }
 }
 

@@ -319,18 +319,18 @@ CESS_HD void inv12(const S& f) {
 // once in the code object; the hard part's five cyclotomic exponentiations by
 // x are spelled out as square runs and multiplies by the base.
 // ---------------------------------------------------------------------------
-enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_END };
-enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6, SL_N };
+enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_CHAIN, FE_END };
+enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6,
+                        SL_X0, SL_X1, SL_X2, SL_X3, SL_X4, SL_X5, SL_N };
 
 // a^x (x = -0xd201000000010000) for a in slot s: |x| has bits 63, 62, 60, 57,
-// 48, 16, so the bits below the top one give Granger-Scott square runs of
-// 1, 2, 3, 9, 32, 16 interleaved with multiplies by the base.  (Karabina's
-// compressed squaring saves a third of the products of a run, but each of the
-// five exponentiations then needs one Fp2 inversion to decompress its six
-// powers, ~460 multiplies: no net gain -- DESIGN.md §5.)
+// 48, 16, so a^|x| = a^(2^63) a^(2^62) a^(2^60) a^(2^57) a^(2^48) a^(2^16).
+// FE_CHAIN s runs the 63 squarings in Karabina's compressed form and leaves
+// the six powers, decompressed with one Fp2 inversion, in slots X5..X0; five
+// multiplies and the conjugation (x < 0) follow.
 #define CESS_FE_CYCEXP(s) \
-  {FE_LOAD, s}, {FE_SQN, 1}, {FE_MUL, s}, {FE_SQN, 2}, {FE_MUL, s}, {FE_SQN, 3}, {FE_MUL, s}, {FE_SQN, 9}, \
-      {FE_MUL, s}, {FE_SQN, 32}, {FE_MUL, s}, {FE_SQN, 16}, {FE_CONJ, 0}
+  {FE_CHAIN, s}, {FE_LOAD, SL_X5}, {FE_MUL, SL_X4}, {FE_MUL, SL_X3}, {FE_MUL, SL_X2}, {FE_MUL, SL_X1}, \
+      {FE_MUL, SL_X0}, {FE_CONJ, 0}
 
 // easy part: m = f^((p^6 - 1)(p^2 + 1)); hard part as in pairing.hpp
 // final_exponentiation (t2 = m).  SL_T0 doubles as scratch in the easy part.
@@ -406,6 +406,132 @@ CESS_HD void cyc_square_run(const A& acc, const P& pk, int n) {
   acc.st(2, z3);
 }
 
+// Karabina compressed squaring (eprint 2010/542) on (z2, z3, z4, z5) (store
+// indices 3, 2, 1, 5; naming as cyc_square_run), which the square's (z2..z5)
+// depend on alone:
+//   z2' = 2 (z2 + 3 xi z4 z5),   z3' = 3 (z4^2 + xi z5^2) - 2 z3,
+//   z4' = 3 (z2^2 + xi z3^2) - 2 z4,   z5' = 2 (z5 + 3 z2 z3),
+// with z4^2 + xi z5^2 = (z4 + z5)(z4 + xi z5) - (1 + xi) z4 z5 (likewise z2, z3):
+// four lazily reduced Fp2 products (3,920 mads) per squaring against
+// Granger-Scott's nine Fp2 squarings (7,056).  z2, z3 stay in registers, z4, z5
+// in the store `x` (HBM in k_final), and the (z4, z5) half's two results are
+// parked in `pk` (LDS) while the (z2, z3) half runs.
+template <class X, class P>
+CESS_HD void kcyc_run(const X& x, const P& pk, fp2& z2, fp2& z3, int n) {
+#pragma unroll 1
+  for (int r = 0; r < n; r++) {
+    CESS_MEMBAR();
+    {
+      const fp2 b = mul(x.ld(1), x.ld(5));
+      CESS_MEMBAR();
+      const fp2 t = mul(add_nr(x.ld(1), x.ld(5)), add_nr(x.ld(1), mul_nr(x.ld(5))));
+      const fp2 nb = mul_nr(b);
+      pk.st(0, mul3(sub(sub(t, b), nb)));   // 3 (z4^2 + xi z5^2)
+      pk.st(1, mul3(dbl(nb)));              // 6 xi z4 z5
+    }
+    CESS_MEMBAR();
+    {
+      const fp2 b = mul(z2, z3);
+      CESS_MEMBAR();
+      const fp2 t = mul(add_nr(z2, z3), add_nr(z2, mul_nr(z3)));
+      x.st(1, sub(mul3(sub(sub(t, b), mul_nr(b))), dbl(x.ld(1))));
+      x.st(5, add(dbl(x.ld(5)), mul3(dbl(b))));
+    }
+    CESS_MEMBAR();
+    z2 = add(dbl(z2), pk.ld(1));
+    z3 = sub(pk.ld(0), dbl(z3));
+  }
+}
+
+// numerator / denominator of z1 of a compressed cyclotomic element:
+//   z2 != 0: z1 = (xi z5^2 + 3 z4^2 - 2 z3) / (4 z2);  z2 == 0: z1 = 2 z4 z5 / z3
+// (den = 0, i.e. z2 = z3 = 0, cannot be decompressed: the caller falls back)
+CESS_HD void cyc_z1_frac(const fp2& z2, const fp2& z3, const fp2& z4, const fp2& z5, fp2& num, fp2& den) {
+  num = sub(add(mul_nr(sqr(z5)), mul3(sqr(z4))), dbl(z3));
+  den = dbl(dbl(z2));
+  if (is_zero(z2)) {   // divergent, practically never taken
+    num = dbl(mul(z4, z5));
+    den = z3;
+  }
+}
+// z0 = xi (2 z1^2 + z2 z5 - 3 z3 z4) + 1
+CESS_HD fp2 cyc_z0(const fp2& z1, const fp2& z2, const fp2& z3, const fp2& z4, const fp2& z5) {
+  return add(mul_nr(sub(add(dbl(sqr(z1)), mul(z2, z5)), mul3(mul(z3, z4)))), fp2_one());
+}
+
+// FE_CHAIN: the powers a^(2^k), k = 16, 48, 57, 60, 62, 63, of the cyclotomic
+// element a (store `base`) into the stores X(0..5): 63 compressed squarings,
+// then z1 of all six powers with ONE Fp2 inversion (Montgomery's simultaneous
+// inversion: numerators parked in the z1 words, prefix products of the
+// denominators in the z0 words; safegcd inversion), then z0.  A lane whose
+// denominator vanishes (z2 = z3 = 0, e.g. a = 1 from an identity pair) redoes
+// its chain with Granger-Scott squarings (divergent, rare).
+template <class B, class XFn, class P>
+CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
+  {
+    const auto w = X(5);   // z4, z5 of the running power
+    w.st(1, base.ld(1));
+    w.st(5, base.ld(5));
+    fp2 z2 = base.ld(3), z3 = base.ld(2);
+    int k = 0;
+#pragma unroll 1
+    for (int j = 0; j < 6; j++) {
+      const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+      kcyc_run(w, pk, z2, z3, stop - k);
+      k = stop;
+      CESS_MEMBAR();
+      const auto x = X(j);
+      x.st(3, z2);
+      x.st(2, z3);
+      if (j < 5) {
+        x.st(1, w.ld(1));
+        x.st(5, w.ld(5));
+      }
+    }
+  }
+  CESS_MEMBAR();
+  bool degen = false;
+  fp2 prod = fp2_one();
+#pragma unroll 1
+  for (int j = 0; j < 6; j++) {
+    const auto x = X(j);
+    fp2 num, den;
+    cyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
+    const bool z = is_zero(den);
+    degen = degen || z;
+    x.st(4, num);
+    x.st(0, prod);   // product of the denominators before j
+    prod = mul(prod, select(z, fp2_one(), den));
+    CESS_MEMBAR();
+  }
+  fp2 iv = inv(prod);
+#pragma unroll 1
+  for (int j = 5; j >= 0; j--) {
+    const auto x = X(j);
+    fp2 num, den;
+    cyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
+    const fp2 ivj = mul(iv, x.ld(0));   // 1 / den_j
+    iv = mul(iv, select(is_zero(den), fp2_one(), den));
+    CESS_MEMBAR();
+    const fp2 z1 = mul(x.ld(4), ivj);
+    x.st(4, z1);
+    CESS_MEMBAR();
+    x.st(0, cyc_z0(z1, x.ld(3), x.ld(2), x.ld(1), x.ld(5)));
+    CESS_MEMBAR();
+  }
+  if (degen) {   // Granger-Scott squarings with X(5) as the running power
+    const auto w = X(5);
+    copy12(w, base);
+#pragma unroll 1
+    for (int j = 0; j < 5; j++) {
+      const int run = j == 0 ? 16 : j == 1 ? 32 : j == 2 ? 9 : j == 3 ? 3 : 2;
+      cyc_square_run(w, pk, run);
+      copy12(X(j), w);
+    }
+    cyc_square_run(w, pk, 1);
+  }
+}
+
 // Run the program.  The accumulator alternates between the stores acc0 and
 // acc1: FE_MUL writes the product of the current one and a slot into the other
 // (mul12_stream, with the parking store `pk` as its Fp6 temporary); every other
@@ -432,6 +558,7 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
       case FE_CONJ: conj12(acc); break;
       case FE_FROB: frob12(acc, arg); break;
       case FE_INV: inv12(acc); break;
+      case FE_CHAIN: cyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }, pk); break;
       default: break;
     }
   }

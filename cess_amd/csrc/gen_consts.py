@@ -242,6 +242,12 @@ def main():
     arr("EXP_SQRT_RATIO", (P - 3) // 4)
     arr("EXP_INV", P - 2)
     arr("EXP_LEGENDRE", (P - 1) // 2)
+    # safegcd inversion (field.hpp inv): p in 13 x 30-bit limbs, p^-1 mod 2^30,
+    # and R^3 mod p, which turns the integer inverse of a Montgomery value aR
+    # (a^-1 R^-1) back into Montgomery form a^-1 R with one product
+    w("CESS_CONST int32_t P30[13] = {" + ", ".join(str((P >> (30 * i)) & ((1 << 30) - 1)) for i in range(13)) + "};")
+    w(f"CESS_CONST uint32_t PINV30 = 0x{pow(P, -1, 1 << 30):08x}u;")
+    arr("R3", RM ** 3 % P)
     arr("B1", mont(4))
     arr("B1_3", mont(12))
     arr("ISO_A", mont(ISO_A))

@@ -28,5 +28,5 @@ enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
 #define CESS_W_G2 48u          // affine G2
 #define CESS_W_COEFFS 4896u    // 68 x 3 Fp2
 #define CESS_W_FP12 144u
-#define CESS_FE_SLOTS 9u       // HBM Fp12 slots of the final-exponentiation program (bls/staged.hpp):
-                               // 7 temporaries, 2 ping-pong accumulators
+#define CESS_FE_SLOTS 15u      // HBM Fp12 slots of the final-exponentiation program (bls/staged.hpp):
+                               // 7 temporaries, 6 powers of FE_CHAIN, 2 ping-pong accumulators

@@ -43,6 +43,11 @@ void emu_fp2_dot2_mont(const uint32_t* in, uint32_t* out0, uint32_t* out1) {
   memcpy(out1, c1.v, 48);
 }
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
+// safegcd inverse of a Montgomery-domain value in [0, 2p); out canonical Montgomery
+void emu_fp_inv_mont(const uint32_t* a, uint32_t* out) {
+  const fp r = fp_reduce_once(inv(load_raw(a)));
+  memcpy(out, r.v, 48);
+}
 int emu_fp2_sqrt(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {
   fp2 a = {to_mont(load_raw(a0)), to_mont(load_raw(a1))}, r;
   bool ok = sqrt(r, a);

@@ -157,3 +157,27 @@ def test_cpu_baseline_path_codes(vectors):
     codes = (ctypes.c_uint8 * n)()
     cpu.cpu_verify_batch(ctypes.c_uint64(n), sigs, msgs, ctypes.c_uint32(32), pks, codes, ctypes.c_int(4))
     assert list(codes) == [c["code"] for c in cases]
+
+
+def test_fp_inv_safegcd(emu):
+    """field.hpp inv(): Bernstein-Yang safegcd (37 x 30 divsteps) on Montgomery
+    values anywhere in the redundant range [0, 2p) -- 0 and p (both zero) map
+    to 0 -- against Python's modular inverse, including values with long runs
+    of equal bits and the largest/smallest residues."""
+    import random
+
+    import oracle.bls_oracle as o
+    P, RM = o.P, 1 << 392
+    rng = random.Random(5)
+    limbs = lambda v: (ctypes.c_uint32 * 12)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+    val = lambda arr: sum(arr[i] << (32 * i) for i in range(12))
+    cases = [0, 1, 2, 3, P - 1, P, P + 1, 2 * P - 1, (P - 1) // 2, (P + 1) // 2, 1 << 380, (1 << 380) - 1,
+             (1 << 381) - 1 - P, RM % P, pow(RM, -1, P)]
+    cases += [(1 << k) % P for k in range(0, 381, 7)] + [((1 << k) - 1) % P for k in range(1, 381, 11)]
+    cases += [rng.randrange(2 * P) for _ in range(400)]
+    for am in cases:
+        out = (ctypes.c_uint32 * 12)()
+        emu.emu_fp_inv_mont(limbs(am), out)
+        a = am * pow(RM, -1, P) % P          # the field element aR -> a
+        want = 0 if a == 0 else pow(a, -1, P) * RM % P
+        assert val(out) == want, hex(am)

@@ -677,19 +677,8 @@ CESS_HD fp2 mul3(const fp2& a) { return {mul3(a.c0), mul3(a.c1)}; }
 CESS_HD fp2 mul4(const fp2& a) { return {mul4(a.c0), mul4(a.c1)}; }
 CESS_HD fp2 mul8(const fp2& a) { return {mul8(a.c0), mul8(a.c1)}; }
 
-// Inputs may be unreduced (each component < 4p, from add_nr): only mul() and
-// add_nr() touch them, and every output is reduced.
-//
-// Lazy reduction: the three Karatsuba products v0 = a0 b0, v1 = a1 b1 and
-// t = (a0 + a1)(b0 + b1) are accumulated column by column and combined BEFORE
-// reducing, so each output component takes one Montgomery reduction:
-//   c0 = v0 - v1 + M   (M = c::LAZY_M28, a multiple of p whose every column
-//                       dominates the same column of any v1, so no column
-//                       goes negative),
-//   c1 = t - v0 - v1   (the limb sums a0 + a1, b0 + b1 are left uncarried, so
-//                       each column of t is exactly v0 + v1 + cross terms).
-// c0 < 2^770 < p 2^392, so each reduction returns < 2p.  3 x 196 product +
-// 2 x 196 reduction mads = 980 vs 1176 for three separate products.
+// Inputs may be unreduced (each component < 2^384, e.g. add_nr sums): only
+// mul() and add_nr() touch them, and every output is reduced.
 #ifndef CESS_FP2_MUL_LAZY
 #define CESS_FP2_MUL_LAZY 1
 #endif
@@ -702,6 +691,16 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   return {sub(v0, v1), sub(sub(t, v0), v1)};
 }
 #else
+// Lazily reduced schoolbook form: c0 = a0 b0 + a1 (K - b1) and
+// c1 = a0 b1 + a1 b0 (K = c::NEG_K28, digit-wise -b1 mod p), four
+// half-products accumulated straight into the two reduction columns -- no
+// per-column combination of separate sums (64-bit subtractions, each with a
+// carry hazard on gfx950) and no operand digit sums.  Columns stay below
+// 14 x 2^56 x 4 + 2^36 < 2^62; c0 < 2^768 + 2^769 < p R, so each reduction
+// returns < 2p.  1,176 mads against 980 for the lazily reduced Karatsuba form
+// (v0 = a0 b0, v1 = a1 b1, t = (a0 + a1)(b0 + b1) combined per column), but
+// 1,529 VALU instructions against 1,756: k_miller 180.4 -> 170.4, k_final
+// 188.4 -> 183.9 ms per 1 M (profiles/r02o_sweep.txt).
 CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   CESS_COUNT_MUL2();
   fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1;
@@ -709,30 +708,25 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   seq(a1);
   seq(b0);
   seq(b1);
-  uint32_t x0[14], x1[14], y0[14], y1[14], xs[14], ys[14];
+  uint32_t x0[14], x1[14], y0[14], y1[14], y1n[14];
   unpack28(a0, x0);
   unpack28(a1, x1);
   unpack28(b0, y0);
   unpack28(b1, y1);
 #pragma unroll
-  for (int i = 0; i < 14; i++) xs[i] = x0[i] + x1[i], ys[i] = y0[i] + y1[i];
+  for (int i = 0; i < 14; i++) y1n[i] = c::NEG_K28[i] - y1[i];
   fp2 r;
   mont28x2(
       [&](int k, uint64_t& acc0, uint64_t& acc1) {
-        // column k's products start after column k-1's reduction (else the
-        // scheduler hoists independent column sums and runs out of registers)
-        uint64_t v0 = zero_after(acc1), v1 = zero_after(acc0);
 #pragma unroll
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
           if (j < 0 || j >= 14) continue;
-          mac(v0, x0[i], y0[j]);
-          mac(v1, x1[i], y1[j]);
-          mac(acc1, xs[i], ys[j]);
+          mac(acc0, x0[i], y0[j]);
+          mac(acc1, x0[i], y1[j]);
+          mac(acc0, x1[i], y1n[j]);
+          mac(acc1, x1[i], y0[j]);
         }
-        acc0 += v0 + c::LAZY_M28[k];
-        acc0 -= v1;
-        acc1 -= v0 + v1;
       },
       r.c0, r.c1);
   seq(r.c0);
@@ -740,17 +734,13 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   return r;
 }
 #endif
-// a*b + c*d over Fp2 with ONE Montgomery reduction per output component: the
-// two Karatsuba products are accumulated column by column into the same three
-// sums (v0, v1, t) before the lazy combination of mul(fp2, fp2) above, so the
-// pair costs 6 half-products + 2 reductions (1,568 mads) instead of two full
-// products (1,960) and an Fp2 addition.  Same input contract as mul(fp2, fp2)
-// (components < 2^384, e.g. add_nr sums).  Bounds: columns of t stay below
-// 2 x 14 x 2^58 + 14 x 2^56 < 2^63.1; c0 = v0 - v1 + 2 M < 2^771 and
-// c1 = t - v0 - v1 < 2^771, both below p R = 2^772.7, so each reduction
-// returns < 2p.
+// a*b + c*d over Fp2 with ONE Montgomery reduction per output component:
+// the schoolbook form of mul(fp2, fp2) above, 8 half-products straight into
+// the two reduction columns (columns < 14 x 2^56 x 7 + 2^36 < 2^63,
+// c0 < 2^770.6 < p R, so each reduction returns < 2p), against two products
+// (2,352 mads) and an Fp2 addition.  Same input contract as mul(fp2, fp2).
 CESS_HD fp2 dot2(const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
-  CESS_COUNT_HALVES(8);
+  CESS_COUNT_HALVES(8);   // algorithmic work: the Karatsuba form's 6 half-products + 2 reductions
   fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1, c0 = c.c0, c1 = c.c1, d0 = d.c0, d1 = d.c1;
   seq(a0);
   seq(a1);
@@ -760,8 +750,7 @@ CESS_HD fp2 dot2(const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
   seq(c1);
   seq(d0);
   seq(d1);
-  uint32_t xa0[14], xa1[14], yb0[14], yb1[14], xc0[14], xc1[14], yd0[14], yd1[14];
-  uint32_t xas[14], ybs[14], xcs[14], yds[14];
+  uint32_t xa0[14], xa1[14], yb0[14], yb1[14], xc0[14], xc1[14], yd0[14], yd1[14], yb1n[14], yd1n[14];
   unpack28(a0, xa0);
   unpack28(a1, xa1);
   unpack28(b0, yb0);
@@ -771,28 +760,23 @@ CESS_HD fp2 dot2(const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
   unpack28(d0, yd0);
   unpack28(d1, yd1);
 #pragma unroll
-  for (int i = 0; i < 14; i++) {
-    xas[i] = xa0[i] + xa1[i], ybs[i] = yb0[i] + yb1[i];
-    xcs[i] = xc0[i] + xc1[i], yds[i] = yd0[i] + yd1[i];
-  }
+  for (int i = 0; i < 14; i++) yb1n[i] = c::NEG_K28[i] - yb1[i], yd1n[i] = c::NEG_K28[i] - yd1[i];
   fp2 r;
   mont28x2(
       [&](int k, uint64_t& acc0, uint64_t& acc1) {
-        uint64_t v0 = zero_after(acc1), v1 = zero_after(acc0);
 #pragma unroll
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
           if (j < 0 || j >= 14) continue;
-          mac(v0, xa0[i], yb0[j]);
-          mac(v1, xa1[i], yb1[j]);
-          mac(acc1, xas[i], ybs[j]);
-          mac(v0, xc0[i], yd0[j]);
-          mac(v1, xc1[i], yd1[j]);
-          mac(acc1, xcs[i], yds[j]);
+          mac(acc0, xa0[i], yb0[j]);
+          mac(acc1, xa0[i], yb1[j]);
+          mac(acc0, xa1[i], yb1n[j]);
+          mac(acc1, xa1[i], yb0[j]);
+          mac(acc0, xc0[i], yd0[j]);
+          mac(acc1, xc0[i], yd1[j]);
+          mac(acc0, xc1[i], yd1n[j]);
+          mac(acc1, xc1[i], yd0[j]);
         }
-        acc0 += v0 + 2 * c::LAZY_M28[k];
-        acc0 -= v1;
-        acc1 -= v0 + v1;
       },
       r.c0, r.c1);
   seq(r.c0);

@@ -701,7 +701,13 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
 // (v0 = a0 b0, v1 = a1 b1, t = (a0 + a1)(b0 + b1) combined per column), but
 // 1,529 VALU instructions against 1,756: k_miller 180.4 -> 170.4, k_final
 // 188.4 -> 183.9 ms per 1 M (profiles/r02o_sweep.txt).
-CESS_HD fp2 mul(const fp2& a, const fp2& b) {
+// mul_scaled<S>(a, b) = S a b, S <= 3, with a's digits scaled after the unpack
+// (digits < 3 x 2^28: columns < 14 (2^57.6 + 2^58.6) + 2^59.8 < 2^63.3, and
+// S a b < 9 x 2^769 < p R, so the reduction still returns < 2p): the small
+// multiple costs one instruction per digit instead of Fp2 additions.
+template <uint32_t S>
+CESS_HD fp2 mul_scaled(const fp2& a, const fp2& b) {
+  static_assert(S >= 1 && S <= 3, "digit bound");
   CESS_COUNT_MUL2();
   fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1;
   seq(a0);
@@ -714,7 +720,11 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   unpack28(b0, y0);
   unpack28(b1, y1);
 #pragma unroll
-  for (int i = 0; i < 14; i++) y1n[i] = c::NEG_K28[i] - y1[i];
+  for (int i = 0; i < 14; i++) {
+    y1n[i] = c::NEG_K28[i] - y1[i];
+    x0[i] *= S;
+    x1[i] *= S;
+  }
   fp2 r;
   mont28x2(
       [&](int k, uint64_t& acc0, uint64_t& acc1) {
@@ -733,6 +743,7 @@ CESS_HD fp2 mul(const fp2& a, const fp2& b) {
   seq(r.c1);
   return r;
 }
+CESS_HD fp2 mul(const fp2& a, const fp2& b) { return mul_scaled<1>(a, b); }
 #endif
 // a*b + c*d over Fp2 with ONE Montgomery reduction per output component:
 // the schoolbook form of mul(fp2, fp2) above, 8 half-products straight into

@@ -245,7 +245,9 @@ CESS_HD void mul6_stream(LA&& a, LB&& b, SK&& sink) {
 // d <- f * g (Karatsuba over Fp6) with every operand streamed: d must be a
 // store distinct from f and g; t is a one-Fp6 temporary store (3 Fp2, indices
 // 0-2).  t0 = f0 g0 goes to t, t1 = f1 g1 to d.c1, then d.c0 = t0 + v t1 and
-// d.c1 = (f0 + f1)(g0 + g1) - t0 - t1 in place.
+// d.c1 = (f0 + f1)(g0 + g1) - t0 - t1 in place.  (Parking the diagonal products
+// in an HBM slot instead of registers measured slower: k_final 186 vs 173 ms
+// per 1 M, profiles/r02q_sweep.txt.)
 template <class D, class S, class G, class T>
 CESS_HD void mul12_stream(const D& d, const S& f, const G& g, const T& t) {
   mul6_stream([&](int j) { return f.ld(j); }, [&](int j) { return g.ld(j); },
@@ -412,9 +414,12 @@ CESS_HD void cyc_square_run(const A& acc, const P& pk, int n) {
 //   z2' = 2 (z2 + 3 xi z4 z5),   z3' = 3 (z4^2 + xi z5^2) - 2 z3,
 //   z4' = 3 (z2^2 + xi z3^2) - 2 z4,   z5' = 2 (z5 + 3 z2 z3),
 // with z4^2 + xi z5^2 = (z4 + z5)(z4 + xi z5) - (1 + xi) z4 z5 (likewise z2, z3):
-// four lazily reduced Fp2 products (3,920 mads) per squaring against
-// Granger-Scott's nine Fp2 squarings (7,056).  z2, z3 stay in registers, z4, z5
-// in the store `x` (HBM in k_final), and the (z4, z5) half's two results are
+// four lazily reduced Fp2 products per squaring against Granger-Scott's nine
+// Fp2 squarings.  The factor 3 of both products of a half rides in the digits
+// of one operand (mul_scaled<3>), so b3 = 3 z4 z5 and t3 = 3 (z4 + z5)(z4 + xi
+// z5) give 3 (z4^2 + xi z5^2) = t3 - b3 - xi b3 and 6 xi z4 z5 = 2 xi b3 with
+// four Fp2 additions instead of seven.  z2, z3 stay in registers, z4, z5 in
+// the store `x` (HBM in k_final), and the (z4, z5) half's two results are
 // parked in `pk` (LDS) while the (z2, z3) half runs.
 template <class X, class P>
 CESS_HD void kcyc_run(const X& x, const P& pk, fp2& z2, fp2& z3, int n) {
@@ -422,20 +427,20 @@ CESS_HD void kcyc_run(const X& x, const P& pk, fp2& z2, fp2& z3, int n) {
   for (int r = 0; r < n; r++) {
     CESS_MEMBAR();
     {
-      const fp2 b = mul(x.ld(1), x.ld(5));
+      const fp2 b3 = mul_scaled<3>(x.ld(1), x.ld(5));
       CESS_MEMBAR();
-      const fp2 t = mul(add_nr(x.ld(1), x.ld(5)), add_nr(x.ld(1), mul_nr(x.ld(5))));
-      const fp2 nb = mul_nr(b);
-      pk.st(0, mul3(sub(sub(t, b), nb)));   // 3 (z4^2 + xi z5^2)
-      pk.st(1, mul3(dbl(nb)));              // 6 xi z4 z5
+      const fp2 t3 = mul_scaled<3>(add_nr(x.ld(1), x.ld(5)), add_nr(x.ld(1), mul_nr(x.ld(5))));
+      const fp2 nb3 = mul_nr(b3);
+      pk.st(0, sub(sub(t3, b3), nb3));   // 3 (z4^2 + xi z5^2)
+      pk.st(1, dbl(nb3));                // 6 xi z4 z5
     }
     CESS_MEMBAR();
     {
-      const fp2 b = mul(z2, z3);
+      const fp2 b3 = mul_scaled<3>(z2, z3);
       CESS_MEMBAR();
-      const fp2 t = mul(add_nr(z2, z3), add_nr(z2, mul_nr(z3)));
-      x.st(1, sub(mul3(sub(sub(t, b), mul_nr(b))), dbl(x.ld(1))));
-      x.st(5, add(dbl(x.ld(5)), mul3(dbl(b))));
+      const fp2 t3 = mul_scaled<3>(add_nr(z2, z3), add_nr(z2, mul_nr(z3)));
+      x.st(1, sub(sub(sub(t3, b3), mul_nr(b3)), dbl(x.ld(1))));   // 3 (z2^2 + xi z3^2) - 2 z4
+      x.st(5, dbl(add(x.ld(5), b3)));                             // 2 (z5 + 3 z2 z3)
     }
     CESS_MEMBAR();
     z2 = add(dbl(z2), pk.ld(1));
@@ -454,9 +459,12 @@ CESS_HD void cyc_z1_frac(const fp2& z2, const fp2& z3, const fp2& z4, const fp2&
     den = z3;
   }
 }
-// z0 = xi (2 z1^2 + z2 z5 - 3 z3 z4) + 1
+// the denominator alone (backward pass of cyc_chain)
+CESS_HD fp2 cyc_z1_den(const fp2& z2, const fp2& z3) { return is_zero(z2) ? z3 : dbl(dbl(z2)); }
+// z0 = xi (2 z1^2 + z2 z5 - 3 z3 z4) + 1, with z2 z5 - 3 z3 z4 as one dot2
+// (one reduction per component instead of two products and a subtraction)
 CESS_HD fp2 cyc_z0(const fp2& z1, const fp2& z2, const fp2& z3, const fp2& z4, const fp2& z5) {
-  return add(mul_nr(sub(add(dbl(sqr(z1)), mul(z2, z5)), mul3(mul(z3, z4)))), fp2_one());
+  return add(mul_nr(add(dbl(sqr(z1)), dot2(z2, z5, neg(mul3(z3)), z4))), fp2_one());
 }
 
 // FE_CHAIN: the powers a^(2^k), k = 16, 48, 57, 60, 62, 63, of the cyclotomic
@@ -508,8 +516,7 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
 #pragma unroll 1
   for (int j = 5; j >= 0; j--) {
     const auto x = X(j);
-    fp2 num, den;
-    cyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
+    const fp2 den = cyc_z1_den(x.ld(3), x.ld(2));
     const fp2 ivj = mul(iv, x.ld(0));   // 1 / den_j
     iv = mul(iv, select(is_zero(den), fp2_one(), den));
     CESS_MEMBAR();

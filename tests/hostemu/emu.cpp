@@ -26,6 +26,14 @@ void emu_fp2_mul_mont(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0
   memcpy(out0, c0.v, 48);
   memcpy(out1, c1.v, 48);
 }
+// 3 a b (mul_scaled<3>: a's digits tripled) on raw (< 2^384) limbs
+void emu_fp2_mul3_mont(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
+                       uint32_t* out0, uint32_t* out1) {
+  fp2 r = mul_scaled<3>(fp2{load_raw(a0), load_raw(a1)}, fp2{load_raw(b0), load_raw(b1)});
+  const fp c0 = fp_reduce_once(r.c0), c1 = fp_reduce_once(r.c1);
+  memcpy(out0, c0.v, 48);
+  memcpy(out1, c1.v, 48);
+}
 // lazily reduced Fp2 square and dot2 on raw (possibly unreduced, < 2^384) limbs
 void emu_fp2_sqr_mont(const uint32_t* a0, const uint32_t* a1, uint32_t* out0, uint32_t* out1) {
   fp2 r = sqr(fp2{load_raw(a0), load_raw(a1)});

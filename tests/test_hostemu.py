@@ -84,7 +84,8 @@ def test_fp2_sqrt_against_oracle(emu):
 
 def test_fp2_mul_lazy_bounds(emu):
     """The lazily reduced Fp2 product (field.hpp mul(fp2, fp2): one Montgomery
-    reduction per component over combined column sums) at the extremes of its
+    reduction per component over combined column sums) and its digit-scaled
+    form mul_scaled<3> at the extremes of its
     input contract -- components up to 2^384 - 1 (unreduced add_nr sums), 0,
     p, multiples of p -- and random values; output must be fully reduced."""
     import random
@@ -104,6 +105,9 @@ def test_fp2_mul_lazy_bounds(emu):
         emu.emu_fp2_mul_mont(limbs(a0), limbs(a1), limbs(b0), limbs(b1), r0, r1)
         assert val(r0) == (a0 * b0 - a1 * b1) * RINV % P, (a0, a1, b0, b1)
         assert val(r1) == (a0 * b1 + a1 * b0) * RINV % P, (a0, a1, b0, b1)
+        emu.emu_fp2_mul3_mont(limbs(a0), limbs(a1), limbs(b0), limbs(b1), r0, r1)   # mul_scaled<3>
+        assert val(r0) == 3 * (a0 * b0 - a1 * b1) * RINV % P, (a0, a1, b0, b1)
+        assert val(r1) == 3 * (a0 * b1 + a1 * b0) * RINV % P, (a0, a1, b0, b1)
 
 
 def test_fp2_sqr_and_dot2_lazy_bounds(emu):

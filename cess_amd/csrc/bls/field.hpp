@@ -273,10 +273,11 @@ CESS_HD fp pack28(const uint32_t (&l)[14]) {
 }
 
 // Montgomery reduction tail shared by mul and sqr:
-//   columns k of the double-width product are accumulated by `col(k, acc)`.
+//   columns k of the double-width product are accumulated by `col(k, acc)`;
+//   the result (< 2p) is left in 14 x 28-bit digits t.
 template <class Col>
-CESS_HD fp mont28(Col&& col) {
-  uint32_t m[14], t[14];
+CESS_HD void mont28_d(Col&& col, uint32_t (&t)[14]) {
+  uint32_t m[14];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 14; k++) {
@@ -296,6 +297,11 @@ CESS_HD fp mont28(Col&& col) {
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;   // result < 2p < 2^382: fits
+}
+template <class Col>
+CESS_HD fp mont28(Col&& col) {
+  uint32_t t[14];
+  mont28_d(col, t);
   return pack28(t);
 }
 
@@ -397,17 +403,72 @@ CESS_HD fp to_mont(const fp& a_raw) { return mul(a_raw, fp_from(c::R2)); }
 // to scratch).  For the 379-381-bit exponents used here (p-2, (p+1)/4,
 // (p-3)/4; ~229 set bits) this is ~110 multiplies instead of ~229.  All
 // branches depend on the exponent only, so they are wave-uniform.
+// The chain runs in the 28-bit digit domain: a Montgomery product's digits
+// (< 2^28, value < 2p) are a valid operand of the next product as they are, so
+// the 12 x 32-bit pack / unpack of every multiply (~70 instructions) is paid
+// once per exponentiation.
+#if defined(CESS_HOSTEMU)
+CESS_HD void seq14(uint32_t (&)[14]) {}
+#else
+CESS_HD void seq14(uint32_t (&x)[14]) {
+  asm volatile(""
+               : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                 "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]));
+}
+#endif
+// r = x y / R on digits (r may alias x or y)
+CESS_HD void mul_d(uint32_t (&r)[14], const uint32_t (&x)[14], const uint32_t (&y)[14]) {
+  CESS_COUNT_MUL();
+  uint32_t t[14];
+  mont28_d(
+      [&](int k, uint64_t& acc) {
+#pragma unroll
+        for (int i = 0; i < 14; i++)
+          if (k - i >= 0 && k - i < 14) mac(acc, x[i], y[k - i]);
+      },
+      t);
+#pragma unroll
+  for (int i = 0; i < 14; i++) r[i] = t[i];
+  seq14(r);
+}
+// x = x^2 / R on digits
+CESS_HD void sqr_d(uint32_t (&x)[14]) {
+  CESS_COUNT_SQR();
+  uint32_t x2[14], t[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) x2[i] = x[i] << 1;
+  mont28_d(
+      [&](int k, uint64_t& acc) {
+#pragma unroll
+        for (int i = 0; i < 14; i++) {
+          const int j = k - i;
+          if (j > i && j < 14) mac(acc, x[i], x2[j]);
+        }
+        if ((k & 1) == 0 && (k >> 1) < 14) mac(acc, x[k >> 1], x[k >> 1]);
+      },
+      t);
+#pragma unroll
+  for (int i = 0; i < 14; i++) x[i] = t[i];
+  seq14(x);
+}
 CESS_HD uint32_t exp_bit(const uint32_t (&e)[12], int i) { return (e[i >> 5] >> (i & 31)) & 1u; }
-CESS_HD fp pow_fixed(const fp& a, const uint32_t (&e)[12]) {
-  const fp a2 = sqr(a);
-  const fp t1 = a, t3 = mul(t1, a2), t5 = mul(t3, a2), t7 = mul(t5, a2);
-  fp r = fp_one();
+CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
+  fp a = a0;
+  seq(a);
+  uint32_t t1[14], t3[14], t5[14], t7[14], a2[14], r[14], w[14];
+  unpack28(a, t1);
+#pragma unroll
+  for (int q = 0; q < 14; q++) a2[q] = t1[q];
+  sqr_d(a2);
+  mul_d(t3, t1, a2);
+  mul_d(t5, t3, a2);
+  mul_d(t7, t5, a2);
   bool started = false;
   int i = 383;
 #pragma unroll 1
   while (i >= 0) {
     if (!exp_bit(e, i)) {
-      if (started) r = sqr(r);
+      if (started) sqr_d(r);
       i--;
       continue;
     }
@@ -417,14 +478,20 @@ CESS_HD fp pow_fixed(const fp& a, const uint32_t (&e)[12]) {
 #pragma unroll 1
     for (int k = i; k >= j; k--) {
       v = 2 * v + exp_bit(e, k);
-      if (started) r = sqr(r);
+      if (started) sqr_d(r);
     }
-    const fp t = v == 1 ? t1 : v == 3 ? t3 : v == 5 ? t5 : t7;
-    r = started ? mul(r, t) : t;
+#pragma unroll
+    for (int q = 0; q < 14; q++) w[q] = v == 1 ? t1[q] : v == 3 ? t3[q] : v == 5 ? t5[q] : t7[q];
+    if (started) {
+      mul_d(r, r, w);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 14; q++) r[q] = w[q];
+    }
     started = true;
     i = j - 1;
   }
-  return r;
+  return pack28(r);
 }
 
 // --- inversion: Bernstein-Yang safegcd (eprint 2019/266) ----------------------

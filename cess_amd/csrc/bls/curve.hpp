@@ -190,6 +190,26 @@ CESS_HD proj<F> proj_mul_u64_mixed(const F& px, const F& py, uint64_t k) {
   return acc;
 }
 
+// as proj_mul_u64_mixed, with the affine base re-read through q(px, py) at
+// each mixed addition instead of being held in registers across the doublings
+template <class F, class QL>
+CESS_HD proj<F> proj_mul_u64_mixed_ld(QL&& q, uint64_t k) {
+  proj<F> acc = proj_identity<F>();
+  bool started = false;
+#pragma unroll 1
+  for (int b = 63; b >= 0; b--) {
+    if (started) acc = proj_dbl(acc);
+    if ((k >> b) & 1u) {
+      CESS_MEMBAR();
+      F px, py;
+      q(px, py);
+      acc = started ? proj_add_mixed(acc, px, py) : proj<F>{px, py, f_one<F>()};
+      started = true;
+    }
+  }
+  return acc;
+}
+
 constexpr uint64_t BLS_X_ABS = 0xd201000000010000ull;   // x = -BLS_X_ABS
 constexpr uint64_t H_EFF_G1 = 0xd201000000010001ull;    // 1 - x
 
@@ -221,11 +241,22 @@ CESS_HD bool g1_is_torsion_free(const fp& px, const fp& py) {
 // G2: psi(P) == [x]P = -[|x|]P
 CESS_HD fp2 psi_x_coeff() { return {fp_from(c::PSI_X_C0), fp_from(c::PSI_X_C1)}; }
 CESS_HD fp2 psi_y_coeff() { return {fp_from(c::PSI_Y_C0), fp_from(c::PSI_Y_C1)}; }
-CESS_HD bool g2_is_torsion_free(const fp2& px, const fp2& py) {
-  g2p xp = proj_mul_u64_mixed(px, py, BLS_X_ABS);
-  g2p psi = {mul(conj(px), psi_x_coeff()), mul(conj(py), psi_y_coeff()), fp2_one()};
+// `pk`: a store of two Fp2 (ld/st by index 0, 1) that holds the point during
+// the scalar multiplication (LDS in k_decode_pk: 48 registers fewer live)
+template <class Park>
+CESS_HD bool g2_is_torsion_free(const fp2& px, const fp2& py, const Park& pk) {
+  pk.st(0, px);
+  pk.st(1, py);
+  g2p xp = proj_mul_u64_mixed_ld<fp2>([&](fp2& x, fp2& y) { x = pk.ld(0), y = pk.ld(1); }, BLS_X_ABS);
+  CESS_MEMBAR();
+  g2p psi = {mul(conj(pk.ld(0)), psi_x_coeff()), mul(conj(pk.ld(1)), psi_y_coeff()), fp2_one()};
   return proj_eq(psi, proj_neg(xp));
 }
+struct RegPark2 {   // register-held store for g2_is_torsion_free (host emulation)
+  fp2 v[2];
+  CESS_HD fp2 ld(int k) const { return v[k]; }
+  CESS_HD void st(int k, const fp2& a) const { const_cast<RegPark2*>(this)->v[k] = a; }
+};
 
 // ---------------------------------------------------------------------------
 // ZCash compressed encodings
@@ -263,7 +294,8 @@ CESS_HD bool g1_decompress(const uint32_t* w, g1a& out) {
   return true;
 }
 
-CESS_HD bool g2_decompress(const uint32_t* w, g2a& out) {
+template <class Park>
+CESS_HD bool g2_decompress(const uint32_t* w, g2a& out, const Park& pk) {
   uint32_t flags = w[0] >> 29;
   bool cflag = flags & 4, iflag = flags & 2, sflag = flags & 1;
   fp x1r = raw_from_be_words(w);
@@ -283,11 +315,13 @@ CESS_HD bool g2_decompress(const uint32_t* w, g2a& out) {
   fp2 y;
   if (!sqrt(y, add(mul(sqr(x), x), b2))) return false;
   if (lex_largest(y) != sflag) y = neg(y);
-  if (!g2_is_torsion_free(x, y)) return false;
-  out.x = x;
-  out.y = y;
+  if (!g2_is_torsion_free(x, y, pk)) return false;
+  CESS_MEMBAR();
+  out.x = pk.ld(0);
+  out.y = pk.ld(1);
   return true;
 }
+CESS_HD bool g2_decompress(const uint32_t* w, g2a& out) { return g2_decompress(w, out, RegPark2{}); }
 
 CESS_HD void g1_compress(const g1a& p, uint8_t* out) {
   if (p.inf) {

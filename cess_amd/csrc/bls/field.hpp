@@ -38,6 +38,14 @@
 
 #include "consts.hpp"
 
+#if defined(CESS_HOSTEMU)
+#define CESS_MEMBAR() ((void)0)
+#else
+// compiler-only barrier: LDS/HBM operands are re-read after it instead of being
+// kept live in registers across phases (register working set control)
+#define CESS_MEMBAR() asm volatile("" ::: "memory")
+#endif
+
 namespace bls {
 
 #if defined(CESS_COUNT_OPS)

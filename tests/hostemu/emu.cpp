@@ -4,6 +4,7 @@
 #include <string.h>
 #include "../../cess_amd/csrc/bls/h2c.hpp"
 #include "../../cess_amd/csrc/bls/staged.hpp"
+#include "../../tools/experimental/miller2.hpp"   // measured slower, kept verified
 
 using namespace bls;
 
@@ -148,6 +149,35 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
   snap(5);
 }
 #endif
+
+// 1 if the two-wave ping-pong Miller loop (miller2.hpp) gives the same Fp12 as
+// the one-wave in-place loop (staged.hpp) on a decodable record, 0 if not,
+// -1 if the record does not decode
+int emu_miller_pp_matches(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk) {
+  init_neg_g2();
+  uint32_t ws[12], wp[24];
+  be_words(sig, 12, ws);
+  be_words(pk, 24, wp);
+  g1a s;
+  g2a q;
+  if (!g1_decompress(ws, s) || !g2_decompress(wp, q)) return -1;
+  g1a h = hash_to_g1(msg, mlen);
+  static coeff3 pkc[N_COEFFS];
+  fp2 qx = q.inf ? fp2{fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)} : q.x;
+  fp2 qy = q.inf ? fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)} : q.y;
+  g2_prepare(qx, qy, [](int i, const coeff3& k) { pkc[i] = k; });
+  static g1a pts[2];
+  pts[0] = s;
+  pts[1] = h;
+  static fp12 f1, fa, fb, t;
+  const bool u0 = !s.inf, u1 = !(q.inf || h.inf);
+  miller_loop2_staged(ArrF12{&f1}, u0, u1, [](int pair) { return pts[pair]; },
+                      [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+  const int w = miller_loop2_pp([](int k) { return ArrF12{k ? &fb : &fa}; }, ArrF12{&t}, u0, u1,
+                                [](int pair) { return pts[pair]; },
+                                [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+  return eq(f1, w ? fb : fa) ? 1 : 0;
+}
 
 // full per-signature verification with the kernel algorithms; gt_out (576 B) optional
 int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {

@@ -68,8 +68,11 @@ CESS_HD bool loop_bit(int b) { return b == 61 || b == 59 || b == 56 || b == 47 |
 constexpr int N_COEFFS = 68;
 
 // G2Prepared: sink(index, coeff3) receives the 68 triples in Miller-loop order.
+// The iteration is the double-and-add of [|x|]Q (63 doublings, additions at
+// |x|'s set bits 62, 60, 57, 48, 16), so on return `t` (optional) holds
+// T = [|x|]Q in Jacobian coordinates.
 template <class Sink>
-CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink) {
+CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink, g2p* t = nullptr) {
   g2p r = {qx, qy, fp2_one()};
   int idx = 0;
 #pragma unroll 1
@@ -78,6 +81,7 @@ CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink) {
     if (loop_bit(b)) sink(idx++, addition_step(r, qx, qy));
   }
   sink(idx++, doubling_step(r));
+  if (t) *t = r;
 }
 
 // Scale a line by 1/c2: (c0, c1, c2) -> (c0/c2, c1/c2, 1).  Every Fp2 factor of

@@ -167,7 +167,7 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
     return CESS_BLS_E_HIP;
   }
   hipLaunchKernelGGL(k_prepare, dim3(1), dim3(64), 0, c->stream, (uint64_t)1, tmp.as<uint32_t>(), c->neg_g2.as<uint4>(),
-                     (uint64_t)1);
+                     (uint64_t)1, (uint8_t*)nullptr, (const uint8_t*)nullptr);
   hipLaunchKernelGGL(k_norm_lines, dim3(1), dim3(128), 0, c->stream, c->neg_g2.as<uint4>());
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     cess_bls_ctx_destroy(c);
@@ -286,7 +286,7 @@ int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8
     LAUNCH(ST_HASH, t, k_hash, dim3(g), dim3(kBlock), 0, t, m, msgs, offs + off, (const uint8_t*)(codes + off),
            S.h_aff.as<uint32_t>(), q);
     LAUNCH(ST_PREPARE, t, k_prepare, dim3(g), dim3(kBlock), 0, t, m, (const uint32_t*)S.pk_aff.as<uint32_t>(),
-           S.coeffs.as<uint4>(), q);
+           S.coeffs.as<uint4>(), q, codes + off, (const uint8_t*)inf);
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;
   };
@@ -529,7 +529,8 @@ int cess_keys_load_one(cess_bls_ctx* c, size_t k, const uint8_t* pks, uint8_t* k
                      (const uint8_t*)nullptr, c->key_code.as<uint8_t>(), c->key_inf.as<uint8_t>(),
                      c->key_aff.as<uint32_t>(), (uint64_t)k, strict);
   hipLaunchKernelGGL(k_prepare, dim3(grid_for(k)), dim3(kBlock), 0, s, (uint64_t)k,
-                     (const uint32_t*)c->key_aff.as<uint32_t>(), c->key_coeffs.as<uint4>(), (uint64_t)k);
+                     (const uint32_t*)c->key_aff.as<uint32_t>(), c->key_coeffs.as<uint4>(), (uint64_t)k,
+                     c->key_code.as<uint8_t>(), (const uint8_t*)c->key_inf.as<uint8_t>());
   HIPCHK(hipGetLastError());
   if (key_codes_out) HIPCHK(hipMemcpyAsync(key_codes_out, c->key_code.p, k, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));

@@ -261,7 +261,8 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
                      (const uint8_t*)nullptr, R.pk_code.as<uint8_t>(), R.pk_inf.as<uint8_t>(), R.pk_aff.as<uint32_t>(),
                      (uint64_t)K, strict);
   hipLaunchKernelGGL(k_prepare, dim3(grid_for(K)), dim3(kBlock), 0, s, (uint64_t)K,
-                     (const uint32_t*)R.pk_aff.as<uint32_t>(), R.pk_coeffs.as<uint4>(), (uint64_t)K);
+                     (const uint32_t*)R.pk_aff.as<uint32_t>(), R.pk_coeffs.as<uint4>(), (uint64_t)K,
+                     R.pk_code.as<uint8_t>(), (const uint8_t*)R.pk_inf.as<uint8_t>());
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(pkc.data(), R.pk_code.p, K, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(pki.data(), R.pk_inf.p, K, hipMemcpyDeviceToHost, s));

@@ -58,9 +58,9 @@ __global__ CESS_LB void k_decode_pk(uint64_t n, const uint8_t* __restrict__ pks,
 #pragma unroll
       for (int k = 0; k < 24; k++) w[k] = bswap(src[k]);
       g2a d;
-      // the point is parked in LDS during the subgroup check's scalar multiplication
-      __shared__ uint4 park[12][256];
-      if (!g2_decompress(w, d, LdsF12{park, threadIdx.x})) c = CODE_PK_POINT;
+      // on-curve decode only: the subgroup check runs in k_prepare, on the
+      // [|x|]Q its G2Prepared iteration computes anyway
+      if (!g2_decompress(w, d, RegPark2{}, false)) c = CODE_PK_POINT;
       else if (d.inf) {
         // the reference accepts the identity key (src/lib.rs:68-82); the
         // optional strict mode rejects it as KeyValidate does

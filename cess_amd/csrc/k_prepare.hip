@@ -9,13 +9,29 @@
 using namespace bls;
 using namespace cess;
 
+// The key's subgroup check (G2Affine::from_compressed's torsion check, A5) is
+// done here: the G2Prepared iteration computes T = [|x|]Q anyway, and
+// psi(Q) == -T is the check k_decode_pk used to run as a second scalar
+// multiplication.  code/inf (null for the -G2 table): a key whose record still
+// has code 0 and is not the identity is rejected as PK_POINT here, after the
+// signature's code (precedence of src/lib.rs:244-245 unchanged: k_decode_pk and
+// this kernel only touch records whose code is still 0).
 __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_aff,
-                                  uint4* __restrict__ coeffs, uint64_t stride) {
+                                  uint4* __restrict__ coeffs, uint64_t stride, uint8_t* __restrict__ code,
+                                  const uint8_t* __restrict__ inf) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  fp2 qx = ld_fp2(pk_aff, stride, i);
-  fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
-  g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); });
+  g2p t;
+  {
+    fp2 qx = ld_fp2(pk_aff, stride, i);
+    fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
+    g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); }, &t);
+  }
+  if (code && code[i] == 0 && !(inf[i] & INF_PK)) {
+    CESS_MEMBAR();
+    if (!g2_psi_is_neg_jacobian(ld_fp2(pk_aff, stride, i), ld_fp2(pk_aff + 24 * stride, stride, i), t.x, t.y, t.z))
+      code[i] = CODE_PK_POINT;
+  }
 }
 
 // The constant -G2 table (one lane per line, stride 1): scale every line to

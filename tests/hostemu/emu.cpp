@@ -179,6 +179,22 @@ int emu_miller_pp_matches(const uint8_t* sig, const uint8_t* msg, uint32_t mlen,
   return eq(f1, w ? fb : fa) ? 1 : 0;
 }
 
+// G2 key acceptance two ways: 1 accept, 0 reject, 2 identity.
+// split = 1: as the kernels do it -- k_decode_pk's on-curve decode, then
+// k_prepare's psi(Q) == -T check on the [|x|]Q of the G2Prepared iteration;
+// split = 0: g2_decompress with its own scalar-multiplication subgroup check
+int emu_g2_accept(const uint8_t* pk, int split) {
+  uint32_t wp[24];
+  be_words(pk, 24, wp);
+  g2a q;
+  if (!split) return g2_decompress(wp, q) ? (q.inf ? 2 : 1) : 0;
+  if (!g2_decompress(wp, q, RegPark2{}, false)) return 0;
+  if (q.inf) return 2;
+  g2p t;
+  g2_prepare(q.x, q.y, [](int, const coeff3&) {}, &t);
+  return g2_psi_is_neg_jacobian(q.x, q.y, t.x, t.y, t.z) ? 1 : 0;
+}
+
 // full per-signature verification with the kernel algorithms; gt_out (576 B) optional
 int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {
   init_neg_g2();

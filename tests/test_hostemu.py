@@ -198,3 +198,37 @@ def test_miller_pingpong_matches_inplace(emu, vectors):
         assert r != 0, c["name"]
         n += r == 1
     assert n >= 8
+
+
+def test_g2_subgroup_check_via_prepare(emu, vectors):
+    """The kernels split G2Affine::from_compressed: k_decode_pk decodes the
+    on-curve point, k_prepare checks psi(Q) == -[|x|]Q on the T its
+    G2Prepared iteration ends with.  Same acceptance as the one-piece decode
+    (and the oracle) on every golden key and on random on-curve points outside
+    G2 (cofactor not cleared), including their negations."""
+    import random
+
+    import oracle.bls_oracle as o
+    seen = set()
+    for c in vectors["cases"]:
+        k = bytes.fromhex(c["pk"])
+        if len(k) != 96 or k in seen:
+            continue
+        seen.add(k)
+        assert emu.emu_g2_accept(k, 1) == emu.emu_g2_accept(k, 0), c["name"]
+    rng = random.Random(17)
+    B2 = (4, 4)
+    bad = 0
+    while bad < 12:
+        x = (rng.randrange(o.P), rng.randrange(o.P))
+        rhs = o.f2_add(o.f2_mul(o.f2_sqr(x), x), B2)
+        if not o.f2_is_square(rhs):
+            continue
+        y = o.f2_sqrt(rhs)
+        for pt in ((x, y), (x, o.f2_neg(y))):
+            enc = o.g2_to_compressed(pt)
+            want = 1 if o.g2_in_subgroup(pt) else 0
+            assert emu.emu_g2_accept(enc, 1) == want == emu.emu_g2_accept(enc, 0)
+            bad += want == 0
+    ok = [bytes.fromhex(c["pk"]) for c in vectors["cases"] if c["code"] == 0][:4]
+    assert ok and all(emu.emu_g2_accept(k, 1) in (1, 2) for k in ok)

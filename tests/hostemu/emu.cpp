@@ -128,12 +128,14 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
   g1_decompress(ws, s);
   snap(0);
   g2a q;
-  g2_decompress(wp, q);
+  g2_decompress(wp, q, RegPark2{}, false);   // as k_decode_pk: on-curve decode only
   snap(1);
   g1a h = hash_to_g1(msg, mlen);
   snap(2);
   static coeff3 pkc[N_COEFFS];
-  g2_prepare(q.x, q.y, [](int i, const coeff3& k) { pkc[i] = k; });
+  g2p t;
+  g2_prepare(q.x, q.y, [](int i, const coeff3& k) { pkc[i] = k; }, &t);
+  (void)g2_psi_is_neg_jacobian(q.x, q.y, t.x, t.y, t.z);   // k_prepare's subgroup check
   snap(3);
   // the staged Miller loop and final-exponentiation program the kernels run
   static fp12 slots[SL_N], acc, acc1, park;

@@ -138,3 +138,35 @@ def test_rlc_identity_keys(ctx, vectors):
     assert codes == expect
     assert expect[5] == expect[700] == 0 and expect[1000] == 5
     assert json.dumps(st)
+
+
+def test_g2_subgroup_check_on_prepared_point(ctx):
+    """k_decode_pk decodes keys on-curve only; k_prepare rejects a key whose
+    psi(Q) != -[|x|]Q on the T of its G2Prepared iteration.  Random on-curve
+    G2 points outside the subgroup (cofactor not cleared, oracle-encoded) must
+    come back PK_POINT (4) -- per record and in the keyed batch's key table --
+    while a bad signature's code keeps precedence over the key's and the
+    valid records around them stay 0 (codes equal the oracle's)."""
+    import oracle.bls_oracle as o
+    rng = random.Random(41)
+    bad = []
+    while len(bad) < 6:
+        x = (rng.randrange(o.P), rng.randrange(o.P))
+        rhs = o.f2_add(o.f2_mul(o.f2_sqr(x), x), (4, 4))
+        if not o.f2_is_square(rhs):
+            continue
+        pt = (x, o.f2_sqrt(rhs))
+        if not o.g2_in_subgroup(pt):
+            bad.append(o.g2_to_compressed(pt))
+    sigs, msgs, pks = _signed(ctx, 16, 7)
+    recs = list(zip(sigs, msgs, pks))
+    for j, k in enumerate(bad):
+        recs[2 * j + 1] = (recs[2 * j + 1][0], recs[2 * j + 1][1], k)
+    recs[3] = (recs[3][0][:-1] + bytes([recs[3][0][-1] ^ 1]), recs[3][1], recs[3][2])   # bad sig + bad key
+    want = [o.verify_code(*r) for r in recs]
+    assert want.count(4) == 5 and want[3] in (1, 2)
+    assert list(ctx.verify_codes(recs)) == want
+    # distinct-key table: one bad key among good ones
+    keys = [pks[0], bad[0], pks[2]]
+    kc = ctx.load_keys(keys)
+    assert list(kc) == [0, 4, 0]

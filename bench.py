@@ -160,6 +160,11 @@ def lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
+# resident waves per SIMD of the two Fp12 kernels, fixed by their LDS images
+# (k_miller 144 KiB per block, k_final 72 KiB)
+WAVES_PER_SIMD = {"k_miller": 1, "k_final": 2}
+
+
 def load_opcount():
     with open(os.path.join(ROOT, "profiles", "opcount.json")) as f:
         return json.load(f)
@@ -594,9 +599,15 @@ def main():
         achieved = alg / (dom_ms * 1e-3)
         sha = lib_sha256()
         pmc = load_pmc_traffic(sha)
-        traffic = None
+        traffic = valu_active = None
         if pmc and pmc.get("n") == chunk:
-            traffic = (pmc.get("all", {}).get(dom) or {}).get("hbm_bytes_per_launch")
+            kd = pmc.get("all", {}).get(dom) or {}
+            traffic = kd.get("hbm_bytes_per_launch")
+            # the issue bound the kernels sit on: share of each wave's cycles
+            # with a VALU instruction issued (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
+            # of the same build; x waves per SIMD = SIMD VALU busy share)
+            if kd.get("SQ_WAVE_CYCLES"):
+                valu_active = kd.get("SQ_ACTIVE_INST_VALU", 0.0) / kd["SQ_WAVE_CYCLES"]
         cpu = None
         if world == 1 and args.cpu_sample > 0:
             import random
@@ -637,6 +648,8 @@ def main():
                          "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
                          "frac": achieved / PEAK_MADS, "traffic": traffic,
                          "traffic_source": pmc["_file"] if pmc else None,
+                         "pmc_valu_active_per_wave": valu_active,
+                         "waves_per_simd": WAVES_PER_SIMD.get(dom),
                          "alg_mads_per_sig": (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL,
                          "whole_path_frac": whole_mads * value / world / PEAK_MADS},
             "cpu_baseline": cpu,

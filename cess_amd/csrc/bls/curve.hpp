@@ -294,15 +294,14 @@ CESS_HD bool g1_decompress(const uint32_t* w, g1a& out) {
   return true;
 }
 
-// psi(Q) == [x]Q = -T for T = [|x|]Q in Jacobian coordinates (X/Z^2, Y/Z^3):
-// psi_x Z^2 == X, psi_y Z^3 == -Y, Z != 0.  k_prepare takes T from the G2Prepared
-// iteration, which runs exactly the double-and-add of [|x|]Q (pairing.hpp
-// g2_prepare), so the subgroup check costs ~6 Fp2 products instead of a second
-// 63-doubling scalar multiplication in k_decode_pk.
-CESS_HD bool g2_psi_is_neg_jacobian(const fp2& qx, const fp2& qy, const fp2& X, const fp2& Y, const fp2& Z) {
-  const fp2 z2 = sqr(Z), z3 = mul(z2, Z);
+// psi(Q) == [x]Q = -T for T = [|x|]Q in homogeneous projective coordinates
+// (X/Z, Y/Z): psi_x Z == X, psi_y Z == -Y, Z != 0.  k_prepare takes T from the
+// G2Prepared iteration, which runs exactly the double-and-add of [|x|]Q
+// (pairing.hpp g2_prepare), so the subgroup check costs ~4 Fp2 products
+// instead of a second 63-doubling scalar multiplication in k_decode_pk.
+CESS_HD bool g2_psi_is_neg_proj(const fp2& qx, const fp2& qy, const fp2& X, const fp2& Y, const fp2& Z) {
   const fp2 px = mul(conj(qx), psi_x_coeff()), py = mul(conj(qy), psi_y_coeff());
-  return !is_zero(Z) && eq(mul(px, z2), X) && eq(mul(py, z3), neg(Y));
+  return !is_zero(Z) && eq(mul(px, Z), X) && eq(mul(py, Z), neg(Y));
 }
 
 // subgroup = false: the on-curve point is returned without the psi check

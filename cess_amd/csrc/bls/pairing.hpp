@@ -5,8 +5,8 @@
 //   G2PREPARED_NEG_G lazy_static          :19-21 -> same routine, run once per context
 //   multi_miller_loop(&[(sig,-G2),(H,pk)]) :90-93 -> miller_loop2
 //   .final_exponentiation().is_identity() :93-95 -> final_exponentiation + is_one
-// Line coefficients follow Costello-Lange-Naehrig (eprint 2010/354) Alg. 26/27 in
-// Jacobian coordinates; the line is applied as f * (c2 + (c1*P.x) v + (c0*P.y) v w).
+// Line coefficients: homogeneous projective doubling/addition (below); the line
+// is applied as f * (c2 + (c1*P.x) v + (c0*P.y) v w).
 #pragma once
 #include "curve.hpp"
 
@@ -16,51 +16,49 @@ struct coeff3 {
   fp2 c0, c1, c2;
 };
 
-// R <- 2R (Jacobian), returns the line coefficients
+// Line coefficients are (c0, c1, c2) = (y_P coefficient, x_P coefficient,
+// constant) of the line through the step's points, applied as
+// f * (c2 + (c1 x_P) v + (c0 y_P) v w).  Any Fp2 multiple of a line gives the
+// same Gt (an Fp2 factor dies in the final exponentiation: (p^2 - 1) divides
+// (p^12 - 1)/r), so the steps use homogeneous projective coordinates
+// (x = X/Z, y = Y/Z) and the cheaper formulas of Costello-Lange-Naehrig /
+// Aranha et al. (eprint 2010/526) for E': y^2 = x^3 + b', b' = 4(1 + u),
+// instead of the crate's Jacobian ones; golden Gt bytes pin the result.
+
+// R <- 2R: (X3, Y3, Z3) = 4 (A (B - F), G^2 - 3 E^2, B H) with A = XY/2,
+// B = Y^2, C = Z^2, E = 3 b' C, F = 3E, G = (B + F)/2, H = 2YZ; tangent line
+// Z^2 (2 y y_P - 3 x^2 x_P + 3 x^3 - 2 y^2) = H y_P - 3 X^2 x_P + (B - E)
+// (X^3 / Z = Y^2 - b' Z^2 on the curve).  6 squarings + 3 products.
 CESS_HD coeff3 doubling_step(g2p& r) {
-  fp2 tmp0 = sqr(r.x);
-  fp2 tmp1 = sqr(r.y);
-  fp2 tmp2 = sqr(tmp1);
-  fp2 tmp3 = sub(sub(sqr(add(tmp1, r.x)), tmp0), tmp2);
-  tmp3 = dbl(tmp3);
-  fp2 tmp4 = mul3(tmp0);
-  fp2 tmp6 = add(r.x, tmp4);
-  fp2 tmp5 = sqr(tmp4);
-  fp2 zsq = sqr(r.z);
-  fp2 nx = sub(sub(tmp5, tmp3), tmp3);
-  fp2 nz = sub(sub(sqr(add(r.z, r.y)), tmp1), zsq);
-  fp2 ny = sub(mul(sub(tmp3, nx), tmp4), mul8(tmp2));
-  fp2 t3 = neg(dbl(mul(tmp4, zsq)));
-  fp2 t6 = sub(sub(sub(sqr(tmp6), tmp0), tmp5), mul4(tmp1));
-  fp2 t0 = dbl(mul(nz, zsq));
+  const fp2 B = sqr(r.y), C = sqr(r.z);
+  const fp2 E = mul3(mul4(mul_nr(C)));              // 3 b' Z^2 = 12 (1 + u) Z^2
+  const fp2 F = mul3(E);
+  const fp2 H = sub(sub(sqr(add(r.y, r.z)), B), C);   // 2 Y Z
+  const fp2 J = sqr(r.x);
+  const fp2 A2 = mul(r.x, r.y);                       // 2A
+  const fp2 nx = dbl(mul(A2, sub(B, F)));
+  const fp2 ny = sub(sqr(add(B, F)), mul4(mul3(sqr(E))));
+  const fp2 nz = mul4(mul(B, H));
   r = {nx, ny, nz};
-  return {t0, t3, t6};
+  return {H, neg(mul3(J)), sub(B, E)};
 }
 
-// R <- R + Q (Jacobian R, affine Q), returns the line coefficients
+// R <- R + Q (projective R, affine Q): theta = Y - y_Q Z, lambda = X - x_Q Z,
+// X3 = lambda H, Y3 = theta (G - H) - Y lambda^3, Z3 = Z lambda^3 with
+// G = X lambda^2, H = lambda^3 + Z theta^2 - 2G; chord line
+// lambda y_P - theta x_P + (theta x_Q - lambda y_Q).
 CESS_HD coeff3 addition_step(g2p& r, const fp2& qx, const fp2& qy) {
-  fp2 zsq = sqr(r.z);
-  fp2 ysq = sqr(qy);
-  fp2 t0 = mul(zsq, qx);
-  fp2 t1 = mul(sub(sub(sqr(add(qy, r.z)), ysq), zsq), zsq);
-  fp2 t2 = sub(t0, r.x);
-  fp2 t3 = sqr(t2);
-  fp2 t4 = mul4(t3);
-  fp2 t5 = mul(t4, t2);
-  fp2 t6 = sub(sub(t1, r.y), r.y);
-  fp2 t9 = mul(t6, qx);
-  fp2 t7 = mul(t4, r.x);
-  fp2 nx = sub(sub(sub(sqr(t6), t5), t7), t7);
-  fp2 nz = sub(sub(sqr(add(r.z, t2)), zsq), t3);
-  fp2 t10 = add(qy, nz);
-  fp2 t8 = mul(sub(t7, nx), t6);
-  fp2 ny = sub(t8, dbl(mul(r.y, t5)));
-  t10 = sub(sub(sqr(t10), ysq), sqr(nz));
-  t9 = sub(dbl(t9), t10);
-  fp2 c0 = dbl(nz);
-  fp2 c1 = dbl(neg(t6));
+  const fp2 th = sub(r.y, mul(qy, r.z));
+  const fp2 la = sub(r.x, mul(qx, r.z));
+  const fp2 D = sqr(la);
+  const fp2 E3 = mul(la, D);
+  const fp2 G = mul(r.x, D);
+  const fp2 H = sub(add(E3, mul(r.z, sqr(th))), dbl(G));
+  const fp2 nx = mul(la, H);
+  const fp2 ny = sub(mul(th, sub(G, H)), mul(r.y, E3));
+  const fp2 nz = mul(r.z, E3);
   r = {nx, ny, nz};
-  return {c0, c1, t9};
+  return {la, neg(th), sub(mul(th, qx), mul(la, qy))};
 }
 
 // bits of |x| >> 1 below its leading one (bit 62), from bit 61 down to 0
@@ -70,7 +68,7 @@ constexpr int N_COEFFS = 68;
 // G2Prepared: sink(index, coeff3) receives the 68 triples in Miller-loop order.
 // The iteration is the double-and-add of [|x|]Q (63 doublings, additions at
 // |x|'s set bits 62, 60, 57, 48, 16), so on return `t` (optional) holds
-// T = [|x|]Q in Jacobian coordinates.
+// T = [|x|]Q in homogeneous projective coordinates.
 template <class Sink>
 CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink, g2p* t = nullptr) {
   g2p r = {qx, qy, fp2_one()};

@@ -29,7 +29,7 @@ __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_af
   }
   if (code && code[i] == 0 && !(inf[i] & INF_PK)) {
     CESS_MEMBAR();
-    if (!g2_psi_is_neg_jacobian(ld_fp2(pk_aff, stride, i), ld_fp2(pk_aff + 24 * stride, stride, i), t.x, t.y, t.z))
+    if (!g2_psi_is_neg_proj(ld_fp2(pk_aff, stride, i), ld_fp2(pk_aff + 24 * stride, stride, i), t.x, t.y, t.z))
       code[i] = CODE_PK_POINT;
   }
 }

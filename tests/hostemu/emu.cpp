@@ -135,7 +135,7 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
   static coeff3 pkc[N_COEFFS];
   g2p t;
   g2_prepare(q.x, q.y, [](int i, const coeff3& k) { pkc[i] = k; }, &t);
-  (void)g2_psi_is_neg_jacobian(q.x, q.y, t.x, t.y, t.z);   // k_prepare's subgroup check
+  (void)g2_psi_is_neg_proj(q.x, q.y, t.x, t.y, t.z);   // k_prepare's subgroup check
   snap(3);
   // the staged Miller loop and final-exponentiation program the kernels run
   static fp12 slots[SL_N], acc, acc1, park;
@@ -194,7 +194,7 @@ int emu_g2_accept(const uint8_t* pk, int split) {
   if (q.inf) return 2;
   g2p t;
   g2_prepare(q.x, q.y, [](int, const coeff3&) {}, &t);
-  return g2_psi_is_neg_jacobian(q.x, q.y, t.x, t.y, t.z) ? 1 : 0;
+  return g2_psi_is_neg_proj(q.x, q.y, t.x, t.y, t.z) ? 1 : 0;
 }
 
 // full per-signature verification with the kernel algorithms; gt_out (576 B) optional

@@ -232,7 +232,54 @@ CESS_HD proj<F> proj_mul_scalar_mixed(const F& px, const F& py, const uint32_t (
 // subgroup checks
 // ---------------------------------------------------------------------------
 // G1: phi(P) == -[x^2]P  with phi(x, y) = (beta x, y)   (P affine, not identity)
+// Jacobian coordinates (x = X/Z^2, y = Y/Z^3) on y^2 = x^3 + b: dbl-2009-l
+// (2M + 5S) and madd-2007-bl (7M + 4S), against 6M + 2S / 11M for the
+// complete RCB formulas above.  Incomplete: doubling maps Z = 0 to Z = 0, and
+// a mixed addition of T = +-Q or of T = O gives Z = 0, which then stays 0 --
+// used only where that outcome means "reject" (g1_is_torsion_free).
+CESS_HD g1p jac_dbl(const g1p& p) {
+  const fp A = sqr(p.x), B = sqr(p.y), C = sqr(B);
+  const fp D = dbl(sub(sub(sqr(add(p.x, B)), A), C));
+  const fp E = mul3(A);
+  const fp x3 = sub(sqr(E), dbl(D));
+  const fp y3 = sub(mul(E, sub(D, x3)), mul8(C));
+  const fp z3 = dbl(mul(p.y, p.z));
+  return {x3, y3, z3};
+}
+CESS_HD g1p jac_add_mixed(const g1p& p, const fp& qx, const fp& qy) {
+  const fp z1z1 = sqr(p.z);
+  const fp u2 = mul(qx, z1z1), s2 = mul(qy, mul(p.z, z1z1));
+  const fp h = sub(u2, p.x), hh = sqr(h);
+  const fp i = mul4(hh), j = mul(h, i);
+  const fp r = dbl(sub(s2, p.y));
+  const fp v = mul(p.x, i);
+  const fp x3 = sub(sub(sqr(r), j), dbl(v));
+  const fp y3 = sub(mul(r, sub(v, x3)), dbl(mul(p.y, j)));
+  const fp z3 = sub(sub(sqr(add(p.z, h)), z1z1), hh);
+  return {x3, y3, z3};
+}
+
+// phi(P) == -[x^2]P (phi(x, y) = (beta x, y) acts as [-x^2] on G1): one
+// 128-bit ladder over x^2 = 0xac45a4010001a4020000000100000000 (17 set bits)
+// in Jacobian coordinates with mixed additions of the affine P, then
+// beta x Z^2 == X, y Z^3 == -Y, Z != 0.  A point of order below 2^128 (never
+// in G1, whose order is the 255-bit prime r) drives some step into T = +-P or
+// O, which leaves Z = 0 and is rejected, as it must be.
 CESS_HD bool g1_is_torsion_free(const fp& px, const fp& py) {
+  constexpr uint64_t X2_HI = 0xac45a4010001a402ull, X2_LO = 0x0000000100000000ull;
+  g1p acc = {px, py, fp_one()};
+#pragma unroll 1
+  for (int b = 126; b >= 0; b--) {
+    acc = jac_dbl(acc);
+    const uint64_t w = b >= 64 ? X2_HI : X2_LO;
+    if ((w >> (b & 63)) & 1u) acc = jac_add_mixed(acc, px, py);
+  }
+  const fp z2 = sqr(acc.z), z3 = mul(z2, acc.z);
+  return !is_zero(acc.z) && eq(mul(mul(px, fp_from(c::G1_BETA)), z2), acc.x) && eq(mul(py, z3), neg(acc.y));
+}
+// the complete-formula form (two 64-bit ladders, RCB), kept as the host
+// cross-check of the Jacobian one
+CESS_HD bool g1_is_torsion_free_rcb(const fp& px, const fp& py) {
   g1p xp = proj_mul_u64_mixed(px, py, BLS_X_ABS);   // [|x|]P
   g1p x2p = proj_mul_u64(xp, BLS_X_ABS);           // [x^2]P
   g1p phi = {mul(px, fp_from(c::G1_BETA)), py, fp_one()};

@@ -197,6 +197,13 @@ int emu_g2_accept(const uint8_t* pk, int split) {
   return g2_psi_is_neg_proj(q.x, q.y, t.x, t.y, t.z) ? 1 : 0;
 }
 
+// G1 subgroup check two ways on raw affine (x, y) limbs: Jacobian ladder over
+// x^2 (the kernels') and the complete-formula two-ladder form
+int emu_g1_torsion_free(const uint32_t* x, const uint32_t* y, int rcb) {
+  const fp px = to_mont(load_raw(x)), py = to_mont(load_raw(y));
+  return rcb ? g1_is_torsion_free_rcb(px, py) : g1_is_torsion_free(px, py);
+}
+
 // full per-signature verification with the kernel algorithms; gt_out (576 B) optional
 int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {
   init_neg_g2();

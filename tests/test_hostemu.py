@@ -232,3 +232,30 @@ def test_g2_subgroup_check_via_prepare(emu, vectors):
             bad += want == 0
     ok = [bytes.fromhex(c["pk"]) for c in vectors["cases"] if c["code"] == 0][:4]
     assert ok and all(emu.emu_g2_accept(k, 1) in (1, 2) for k in ok)
+
+
+def test_g1_subgroup_check_jacobian(emu):
+    """field/curve.hpp g1_is_torsion_free: one Jacobian ladder over x^2 with
+    incomplete formulas agrees with the complete-formula form and with the
+    oracle on G1 points, on random on-curve points outside G1 and on points of
+    small order (3-torsion: y^2 = x^3 + 4 has the order-3 points (0, +-2))."""
+    import random
+
+    import oracle.bls_oracle as o
+    rng = random.Random(23)
+    limbs = lambda v: (ctypes.c_uint32 * 12)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+    pts = [(0, 2), (0, o.P - 2)]
+    while len(pts) < 26:
+        x = rng.randrange(o.P)
+        rhs = (x * x * x + 4) % o.P
+        if pow(rhs, (o.P - 1) // 2, o.P) != 1:
+            continue
+        pts.append((x, o.fp_sqrt(rhs)))
+    g = o.G1_GEN if hasattr(o, "G1_GEN") else None
+    if g:
+        for k in (1, 2, 3, 12345, o.R - 1):
+            pts.append(o.ec_mul(o.FP, g, k) if hasattr(o, "FP") else g)
+    for (x, y) in pts:
+        want = 1 if o.g1_in_subgroup((x, y)) else 0
+        assert emu.emu_g1_torsion_free(limbs(x), limbs(y), 0) == want, (x, y)
+        assert emu.emu_g1_torsion_free(limbs(x), limbs(y), 1) == want, (x, y)

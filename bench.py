@@ -73,6 +73,12 @@ def parse():
     ap.add_argument("--forged-count", type=int, default=0, help="forgeries per rank (rlc mode)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rendezvous/sharding only, no GPU (CPU test of the N>1 path)")
+    ap.add_argument("--transport", choices=["rccl", "shm"], default="rccl",
+                    help="communicator of the sharded entry points: rccl (xGMI, one GPU per rank; default) or "
+                         "shm (host shared memory: ranks may share a GPU -- a rehearsal of the N>1 path on one box)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on GPU 0 (with --transport shm: N>1 rehearsal on a one-GPU box; the "
+                         "throughput is then NOT an N-GPU figure)")
     return ap.parse_args(argv)
 
 
@@ -128,10 +134,17 @@ def rdv_cleanup(rank: int, world: int):
         shutil.rmtree(rdv_dir(), ignore_errors=True)
 
 
-def comm_setup(ctx, rank: int, world: int):
-    """ncclUniqueId from rank 0 to every rank (file rendezvous), then
-    ncclCommInitRank inside the library."""
+def comm_setup(ctx, rank: int, world: int, transport: str = "rccl"):
+    """ncclUniqueId (or the shared-memory job name) from rank 0 to every rank
+    (file rendezvous), then the communicator inside the library."""
     from cess_amd import bls
+    if transport == "shm":
+        if rank == 0:
+            rdv_put("comm_name", bls.comm_shm_name().encode())
+        ctx.comm_init_shm(world, rank, rdv_get("comm_name").decode())
+        ctx.comm_barrier()
+        rdv_cleanup(rank, world)
+        return
     if rank == 0:
         rdv_put("comm_id", bls.comm_id())
     cid = rdv_get("comm_id")
@@ -487,7 +500,7 @@ def main():
         sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
         run_dry(args, rank, world)
         return
@@ -501,21 +514,21 @@ def main():
     if args.mode == "rsa":
         ctx = bls.Context(device=local, max_batch=1 << 16)
         if world > 1:
-            comm_setup(ctx, rank, world)
+            comm_setup(ctx, rank, world, args.transport)
         run_rsa(args, ctx, rank, world)
         ctx.close()
         return
     if args.mode == "rlc":
         ctx = bls.Context(device=local, max_batch=min(args.n or (4 << 20), 1 << 20))
         if world > 1:
-            comm_setup(ctx, rank, world)
+            comm_setup(ctx, rank, world, args.transport)
         run_rlc(args, ctx, rank, world)
         ctx.close()
         return
 
     ctx = bls.Context(device=local, max_batch=min(n, 1 << 20), profile=True)
     if world > 1:
-        comm_setup(ctx, rank, world)
+        comm_setup(ctx, rank, world, args.transport)
     n_total = n * world
     keyed = args.mode == "keyed"
     if keyed:
@@ -639,6 +652,8 @@ def main():
             "data": "synthetic: random distinct keys + 32-byte messages, keys/sigs generated on GPU",
             "config": {"workload": wl, "sigs_per_gpu": n, "sigs_total": n_total, "msg_bytes": 32,
                        "forged_frac": args.forged_frac, "parallelism": f"shard-by-index x{world}",
+                       "transport": ctx.comm_kind if world > 1 else None,
+                       "ranks_share_gpu0": bool(args.one_device and world > 1),
                        "launch_chunk": chunk},
             "verdicts_ok": ok,
             "bitmap_popcount": popcount,

@@ -45,6 +45,9 @@ EXPORTS = (
     "cess_bls_comm_max_f64", "cess_bls_device_alloc", "cess_bls_device_free", "cess_bls_copy_to_device",
     "cess_bls_copy_from_device", "cess_bls_synchronize", "cess_bls_enclave_verify_bls",
     "cess_bls_stage_stats", "cess_bls_launch_records",
+    # transport seam of the sharded entry points (RCCL or host shared memory)
+    "cess_bls_comm_kind", "cess_bls_comm_shm_name", "cess_bls_comm_init_shm", "cess_bls_comm_open_shm",
+    "cess_bls_comm_close", "cess_bls_comm_agree", "cess_bls_comm_gather_verdicts",
     # include/cess_rsa.h (RSA PKCS#1 v1.5 raw verify, cp_enclave_verify::verify_rsa)
     "cess_rsa_parse_key", "cess_rsa_keys_load", "cess_rsa_verify_batch", "cess_rsa_verify_batch_device",
     "cess_rsa_verify",
@@ -55,6 +58,7 @@ RSA_CODE_NAMES = {0: "OK", 1: "SIG_LEN", 2: "SIG_RANGE", 3: "MSG_LEN", 4: "MISMA
 
 # infrastructure status codes (include/cess_bls.h)
 E_INVALID_ARG, E_NO_DEVICE, E_HIP, E_OOM, E_RCCL, E_BUSY, E_BAD_KEY, E_BAD_SIG, E_NO_COMM = range(-1, -10, -1)
+E_COMM = -11
 F_PROFILE, F_STRICT_IDENTITY = 1, 2
 MODE_PER_SIG, MODE_RLC = 0, 1
 
@@ -117,6 +121,15 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_verify_batch_sharded_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
         lib.cess_bls_verify_batch_rlc_sharded.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p, _u64p, _u64p,
                                                           ctypes.POINTER(ctypes.c_int)]
+        lib.cess_bls_comm_init_shm.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+        lib.cess_bls_comm_kind.argtypes = [vp]
+        lib.cess_bls_comm_kind.restype = ctypes.c_char_p
+        lib.cess_bls_comm_shm_name.argtypes = [ctypes.c_char_p]
+        lib.cess_bls_comm_open_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        lib.cess_bls_comm_close.argtypes = [vp]
+        lib.cess_bls_comm_close.restype = None
+        lib.cess_bls_comm_agree.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        lib.cess_bls_comm_gather_verdicts.argtypes = [vp, ctypes.c_uint64, _u8p, _u8p, _u64p]
         lib.cess_bls_comm_barrier.argtypes = [vp]
         lib.cess_bls_comm_max_f64.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         lib.cess_bls_device_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
@@ -362,6 +375,16 @@ class Context:
         self._chk(self._lib.cess_bls_comm_init(self._h, nranks, rank, _buf(comm_id)))
         self.nranks, self.rank = nranks, rank
 
+    def comm_init_shm(self, nranks: int, rank: int, name: str):
+        """Host shared-memory transport (ranks on one host, may share a GPU;
+        collective, same name on every rank: comm_shm_name())."""
+        self._chk(self._lib.cess_bls_comm_init_shm(self._h, nranks, rank, name.encode()))
+        self.nranks, self.rank = nranks, rank
+
+    @property
+    def comm_kind(self) -> str:
+        return self._lib.cess_bls_comm_kind(self._h).decode()
+
     def verify_sharded(self, sigs: bytes, pks: bytes, msgs: bytes, msg_offsets) -> Tuple[bytes, list]:
         """Every rank passes the whole fixed-stride batch; returns the verdicts
         of all records (each rank verifies its shard, RCCL all-gathers)."""
@@ -561,6 +584,58 @@ def comm_id() -> bytes:
     if st != 0:
         raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
     return bytes(out)
+
+
+def comm_shm_name() -> str:
+    """A fresh job name for the shared-memory transport; make it on one rank
+    and distribute it out of band (as comm_id for RCCL)."""
+    lib = load_library()
+    out = ctypes.create_string_buffer(64)
+    st = lib.cess_bls_comm_shm_name(out)
+    if st != 0:
+        raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
+    return out.value.decode()
+
+
+class Comm:
+    """Context-free shared-memory communicator (cess_bls_comm_open_shm): the
+    merge step of the sharded entry points.  Needs no GPU."""
+
+    def __init__(self, name: str, nranks: int, rank: int):
+        self._lib = load_library()
+        h = ctypes.c_void_p()
+        st = self._lib.cess_bls_comm_open_shm(name.encode(), nranks, rank, ctypes.byref(h))
+        if st != 0:
+            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode(), st)
+        self._h = h
+        self.nranks, self.rank = nranks, rank
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.cess_bls_comm_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st):
+        if st != 0:
+            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode(), st)
+
+    def agree(self, status: int) -> int:
+        out = ctypes.c_int()
+        self._chk(self._lib.cess_bls_comm_agree(self._h, status, ctypes.byref(out)))
+        return out.value
+
+    def gather_verdicts(self, n_total: int, shard_codes: bytes) -> Tuple[bytes, list]:
+        """(codes, bitmap words) of the whole batch from this rank's shard codes."""
+        codes = (ctypes.c_uint8 * max(n_total, 1))()
+        bitmap = (ctypes.c_uint64 * max((n_total + 63) // 64, 1))()
+        self._chk(self._lib.cess_bls_comm_gather_verdicts(self._h, n_total, _buf(shard_codes), codes, bitmap))
+        return bytes(codes)[:n_total], list(bitmap)[: (n_total + 63) // 64]
 
 
 def default_context() -> Context:

@@ -31,7 +31,8 @@ extern "C" const char* cess_bls_status_string(int s) {
     case CESS_BLS_E_BUSY: return "context in use by another thread";
     case CESS_BLS_E_BAD_KEY: return "public key does not deserialize (verify_bls would panic)";
     case CESS_BLS_E_BAD_SIG: return "signature does not deserialize (verify_bls would panic)";
-    case CESS_BLS_E_NO_COMM: return "no communicator (cess_bls_comm_init)";
+    case CESS_BLS_E_NO_COMM: return "no communicator (cess_bls_comm_init / cess_bls_comm_init_shm)";
+    case CESS_BLS_E_COMM: return "shared-memory communicator failed (peer timeout or transport error)";
     case CESS_RSA_E_UNSUPPORTED: return "RSA modulus longer than 2048 bits (not supported on the GPU)";
   }
   return "unknown status";
@@ -186,7 +187,7 @@ extern "C" void cess_bls_ctx_destroy(cess_bls_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
   }
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
-  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c->xport;
   for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->done_ev, c->ev_start, c->ev_light[0], c->ev_light[1], c->ev_mill[0], c->ev_mill[1]})
     if (e) (void)hipEventDestroy(e);

@@ -13,6 +13,7 @@
 
 #include "../../include/cess_bls.h"
 #include "../../include/cess_rsa.h"
+#include "comm.hpp"
 #include "kernels.hpp"
 
 // kernels (k_*.hip)
@@ -79,6 +80,10 @@ struct RlcState {
   std::vector<uint64_t> gbeg;       // K + 1 group boundaries in perm
   uint32_t K = 0;
   bool local_ok = false;
+  // set only when the most recent rlc_begin completed: rlc_finish refuses
+  // (CESS_BLS_E_INVALID_ARG) otherwise, so a failed or partial begin can never
+  // be finished into "all verified" (fail closed)
+  bool valid = false;
   bool per_sig = false;             // too many distinct keys for a combination: verified per signature
   uint64_t checks = 0, leaves = 0, leaf_sigs = 0;
   DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
@@ -138,8 +143,10 @@ struct cess_bls_ctx {
   // one host thread at a time (the ABI contract); a second concurrent caller
   // gets CESS_BLS_E_BUSY instead of racing on the context buffers
   std::mutex busy;
-  // RCCL communicator (cess_bls_comm_init): one rank per process and GPU
-  ncclComm_t comm = nullptr;
+  // communicator of the sharded entry points (comm.hpp): RCCL
+  // (cess_bls_comm_init, one rank per process and GPU) or host shared memory
+  // (cess_bls_comm_init_shm); owned
+  cess_host::Transport* xport = nullptr;
   int nranks = 1, rank = 0;
   cess_host::DevBuf comm_buf, comm_words, comm_codes;
   // multi-device context (cess_bls_config.n_devices > 1): one sub-context per
@@ -194,8 +201,6 @@ int verify_rlc_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_
                     uint64_t* stats4);
 // OS randomness for RLC seeds drawn by the library (mode = RLC)
 int os_random(uint8_t* out, size_t n);
-// shard of a batch for rank r of R (whole bitmap words, equal word count per rank)
-void shard_of(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end, uint64_t* words_per_rank);
 // bitmap words from codes (host)
 void bitmap_from_codes(const uint8_t* codes, uint64_t n, uint64_t* words);
 

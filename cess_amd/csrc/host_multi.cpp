@@ -3,12 +3,14 @@
 // Signatures are independent (reference src/lib.rs:243 is per signature), so a
 // batch shards by index with no exchange during compute.  Two deployments:
 //
-//  * one process per GPU (cess_bls_comm_init): the context owns an RCCL
-//    communicator; the sharded entry points verify the rank's shard and
-//    all-gather the verdict-bitmap words (and code bytes, and in RLC mode the
-//    576-byte Gt partials) over xGMI with ncclAllGather.  Shards are whole
-//    bitmap words with an equal word count per rank, so the all-gather is in
-//    place and needs no re-packing.
+//  * one process per GPU (cess_bls_comm_init / _init_shm): the context owns a
+//    communicator behind the transport seam of comm.hpp -- RCCL over xGMI in
+//    production, host shared memory for ranks that share a GPU (tests on a
+//    one-GPU box).  The sharded entry points verify the rank's shard, agree on
+//    a status, and all-gather the verdict-bitmap words and code bytes (in RLC
+//    mode the 576-byte Gt partials).  Shards are whole bitmap words with an
+//    equal word count per rank, so the all-gather is in place and needs no
+//    re-packing.
 //  * one process driving several GPUs (cess_bls_config.n_devices > 1): the
 //    context holds one sub-context per device and the host-buffer batches are
 //    split the same way across them, one host thread per device, each writing
@@ -38,7 +40,84 @@ int cess_gen_one(cess_bls_ctx* c, int kind, size_t n, const uint8_t* sks, const 
                  uint8_t* out);
 
 // ---------------------------------------------------------------------------
-// one process per GPU: RCCL communicator
+// RCCL transport (comm.hpp): production, one process per GPU, xGMI
+// ---------------------------------------------------------------------------
+namespace {
+class RcclTransport final : public Transport {
+ public:
+  ~RcclTransport() override {
+    if (ctl_) {
+      (void)hipSetDevice(dev_);
+      (void)hipStreamSynchronize(ctl_);
+    }
+    if (comm_) (void)ncclCommDestroy(comm_);
+    if (ctl_) (void)hipStreamDestroy(ctl_);
+  }
+  const char* kind() const override { return "rccl"; }
+
+  int init(cess_bls_ctx* c, int nranks, int rank, const ncclUniqueId& id) {
+    dev_ = c->device;
+    ctx_ = c;
+    this->nranks = nranks;
+    this->rank = rank;
+    HIPCHK(hipSetDevice(dev_));
+    HIPCHK(hipStreamCreateWithFlags(&ctl_, hipStreamNonBlocking));
+    NCCLCHK(ncclCommInitRank(&comm_, nranks, id, rank));
+    return CESS_BLS_OK;
+  }
+
+  int allgather_dev(int dev, void* dbuf, size_t bytes, hipStream_t s) override {
+    (void)dev;
+    char* b = static_cast<char*>(dbuf);
+    NCCLCHK(ncclAllGather(b + (size_t)rank * bytes, b, bytes, ncclUint8, comm_, s));
+    return CESS_BLS_OK;
+  }
+
+  // Host-side collectives run on the control stream after the context's
+  // previous work (order_begin): RCCL then executes this communicator's
+  // collectives in the order every rank issued them.
+  int allgather_host(void* buf, size_t bytes) override {
+    HIPCHK(hipSetDevice(dev_));
+    int r = order_begin(ctx_, ctl_);
+    if (r) return r;
+    if (buf_.ensure(std::max<size_t>(1, (size_t)nranks * bytes))) return CESS_BLS_E_OOM;
+    char* d = buf_.as<char>();
+    char* h = static_cast<char*>(buf);
+    if (bytes) HIPCHK(hipMemcpyAsync(d + (size_t)rank * bytes, h + (size_t)rank * bytes, bytes, hipMemcpyHostToDevice, ctl_));
+    NCCLCHK(ncclAllGather(d + (size_t)rank * bytes, d, bytes, ncclUint8, comm_, ctl_));
+    if (bytes) HIPCHK(hipMemcpyAsync(h, d, (size_t)nranks * bytes, hipMemcpyDeviceToHost, ctl_));
+    HIPCHK(hipStreamSynchronize(ctl_));
+    return order_end(ctx_, ctl_);
+  }
+
+  int max_i64(int64_t* v, int n) override { return allreduce_max(v, n, ncclInt64); }
+  int max_f64(double* v) override { return allreduce_max(v, 1, ncclFloat64); }
+
+ private:
+  template <class T>
+  int allreduce_max(T* v, int n, ncclDataType_t t) {
+    HIPCHK(hipSetDevice(dev_));
+    int r = order_begin(ctx_, ctl_);
+    if (r) return r;
+    if (buf_.ensure(std::max<size_t>(64, n * sizeof(T)))) return CESS_BLS_E_OOM;
+    T* d = buf_.as<T>();
+    HIPCHK(hipMemcpyAsync(d, v, n * sizeof(T), hipMemcpyHostToDevice, ctl_));
+    NCCLCHK(ncclAllReduce(d, d, n, t, ncclMax, comm_, ctl_));
+    HIPCHK(hipMemcpyAsync(v, d, n * sizeof(T), hipMemcpyDeviceToHost, ctl_));
+    HIPCHK(hipStreamSynchronize(ctl_));
+    return order_end(ctx_, ctl_);
+  }
+
+  int dev_ = 0;
+  cess_bls_ctx* ctx_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t ctl_ = nullptr;
+  DevBuf buf_;
+};
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// communicator setup
 // ---------------------------------------------------------------------------
 extern "C" int cess_bls_shard_range(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end,
                                     uint64_t* words_per_rank) {
@@ -58,60 +137,66 @@ extern "C" int cess_bls_comm_id(uint8_t id_out[CESS_BLS_COMM_ID_BYTES]) {
 
 extern "C" int cess_bls_comm_init(cess_bls_ctx* c, int nranks, int rank, const uint8_t id_in[CESS_BLS_COMM_ID_BYTES]) {
   ENTRY(c);
-  if (!c->subs.empty() || !id_in || nranks <= 0 || rank < 0 || rank >= nranks || c->comm) return CESS_BLS_E_INVALID_ARG;
-  HIPCHK(hipSetDevice(c->device));
+  if (!c->subs.empty() || !id_in || nranks <= 0 || rank < 0 || rank >= nranks || c->xport) return CESS_BLS_E_INVALID_ARG;
   ncclUniqueId id;
   memcpy(&id, id_in, sizeof(id));
-  ncclComm_t comm = nullptr;
-  NCCLCHK(ncclCommInitRank(&comm, nranks, id, rank));
-  c->comm = comm;
+  RcclTransport* t = new RcclTransport();
+  const int r = t->init(c, nranks, rank, id);
+  if (r) {
+    delete t;
+    return r;
+  }
+  c->xport = t;
   c->nranks = nranks;
   c->rank = rank;
   return CESS_BLS_OK;
 }
 
-// all-gather `count` elements per rank in place: rank r's block at buf + r * count
-static int allgather_inplace(cess_bls_ctx* c, void* buf, size_t count, ncclDataType_t t, size_t esize, hipStream_t s) {
-  char* b = static_cast<char*>(buf);
-  NCCLCHK(ncclAllGather(b + (size_t)c->rank * count * esize, b, count, t, c->comm, s));
+extern "C" int cess_bls_comm_init_shm(cess_bls_ctx* c, int nranks, int rank, const char* name) {
+  ENTRY(c);
+  if (!c->subs.empty() || c->xport) return CESS_BLS_E_INVALID_ARG;
+  Transport* t = nullptr;
+  const int r = make_shm_transport(name, nranks, rank, &t);
+  if (r) return r;
+  c->xport = t;
+  c->nranks = nranks;
+  c->rank = rank;
   return CESS_BLS_OK;
 }
 
+extern "C" const char* cess_bls_comm_kind(cess_bls_ctx* c) {
+  return (c && c->xport) ? c->xport->kind() : "none";
+}
+
+// ---------------------------------------------------------------------------
+// sharded entry points
+// ---------------------------------------------------------------------------
+// Every rank runs the same collective sequence whatever happens locally:
+// (1) the batch size must agree, (2) local work, (3) agree() on the worst
+// status -- a failure anywhere returns that failure on every rank, before any
+// data moves -- (4) the data all-gathers.
 extern "C" int cess_bls_verify_batch_sharded(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,
                                              const uint8_t* msgs, const uint64_t* offs, uint8_t* codes_out,
                                              uint64_t* bitmap_out) {
   ENTRY(c);
-  if (!c->comm) return CESS_BLS_E_NO_COMM;
-  if (n && (!sigs || !pks || !offs)) return CESS_BLS_E_INVALID_ARG;
+  if (!c->xport) return CESS_BLS_E_NO_COMM;
+  Transport& t = *c->xport;
   uint64_t b, e, wpr;
   shard_of(n, c->nranks, c->rank, &b, &e, &wpr);
   const uint64_t m = e - b;
-  // the rank's verdicts (host), then one in-place all-gather of words and codes
-  std::vector<uint8_t> codes(std::max<uint64_t>(wpr * 64, 1), 0xff);
-  std::vector<uint64_t> words(std::max<uint64_t>(wpr, 1), 0);
-  int r = CESS_BLS_OK;
-  if (m) r = verify_host(c, m, sigs + 48 * b, pks + 96 * b, msgs, offs + b, nullptr, codes.data(), words.data(), nullptr);
+  // the whole batch is validated on every rank (the same inputs give the same
+  // answer everywhere; agree() covers ranks given different ones)
+  int st = CESS_BLS_OK;
+  if (n && (!sigs || !pks || !offs)) st = CESS_BLS_E_INVALID_ARG;
+  for (uint64_t i = 0; st == CESS_BLS_OK && i < n; i++)
+    if (offs[i + 1] < offs[i]) st = CESS_BLS_E_INVALID_ARG;
+  if (st == CESS_BLS_OK && n && !msgs && offs[n] != offs[0]) st = CESS_BLS_E_INVALID_ARG;
+  std::vector<uint8_t> codes(std::max<uint64_t>(m, 1), 0xff);
+  if (st == CESS_BLS_OK && m)
+    st = verify_host(c, m, sigs + 48 * b, pks + 96 * b, msgs, offs + b, nullptr, codes.data(), nullptr, nullptr);
+  int r = agree(t, st);
   if (r) return r;
-  if (wpr == 0) return CESS_BLS_OK;   // empty batch
-  HIPCHK(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  r = order_begin(c, s);
-  if (r) return r;
-  if (c->comm_words.ensure(c->nranks * wpr * 8) | c->comm_codes.ensure(c->nranks * wpr * 64)) return CESS_BLS_E_OOM;
-  uint64_t* dw = c->comm_words.as<uint64_t>();
-  uint8_t* dc = c->comm_codes.as<uint8_t>();
-  HIPCHK(hipMemcpyAsync(dw + c->rank * wpr, words.data(), wpr * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(dc + c->rank * wpr * 64, codes.data(), wpr * 64, hipMemcpyHostToDevice, s));
-  r = allgather_inplace(c, dw, wpr, ncclUint64, 8, s);
-  if (r) return r;
-  if (codes_out) {
-    r = allgather_inplace(c, dc, wpr * 64, ncclUint8, 1, s);
-    if (r) return r;
-    HIPCHK(hipMemcpyAsync(codes_out, dc, n, hipMemcpyDeviceToHost, s));
-  }
-  if (bitmap_out) HIPCHK(hipMemcpyAsync(bitmap_out, dw, ((n + 63) / 64) * 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return order_end(c, s);
+  return gather_verdicts(t, n, codes.data(), codes_out, bitmap_out);
 }
 
 extern "C" int cess_bls_verify_batch_sharded_device(cess_bls_ctx* c, size_t n_total, const uint8_t* d_sigs,
@@ -119,42 +204,51 @@ extern "C" int cess_bls_verify_batch_sharded_device(cess_bls_ctx* c, size_t n_to
                                                     const uint64_t* d_offs, uint8_t* d_codes_all,
                                                     uint64_t* d_bitmap_all, void* stream) {
   ENTRY(c);
-  if (!c->comm) return CESS_BLS_E_NO_COMM;
-  if (!d_bitmap_all) return CESS_BLS_E_INVALID_ARG;
+  if (!c->xport) return CESS_BLS_E_NO_COMM;
+  Transport& t = *c->xport;
   uint64_t b, e, wpr;
   shard_of(n_total, c->nranks, c->rank, &b, &e, &wpr);
   const uint64_t m = e - b;
-  if (m && (!d_sigs || !d_pks || !d_offs)) return CESS_BLS_E_INVALID_ARG;
-  if (wpr == 0) return CESS_BLS_OK;
-  HIPCHK(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  int r = order_begin(c, s);
+  // (1) + local checks and allocations, then (3): nothing is enqueued before
+  // every rank knows it can run
+  // n_total and whether codes are gathered fix the collective sequence
+  bool same = false;
+  int r = same_on_all_ranks(t, ((uint64_t)n_total << 1) | (d_codes_all ? 1u : 0u), &same);
   if (r) return r;
+  int st = same ? CESS_BLS_OK : CESS_BLS_E_INVALID_ARG;
+  if (!d_bitmap_all || (m && (!d_sigs || !d_pks || !d_offs))) st = CESS_BLS_E_INVALID_ARG;
+  if (st == CESS_BLS_OK && hipSetDevice(c->device) != hipSuccess) st = CESS_BLS_E_HIP;
+  if (st == CESS_BLS_OK && !d_codes_all && c->comm_codes.ensure(std::max<uint64_t>(m, 1))) st = CESS_BLS_E_OOM;
+  r = agree(t, st);
+  if (r) return r;
+  if (wpr == 0) return CESS_BLS_OK;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  r = order_begin(c, s);
   uint64_t* my_words = d_bitmap_all + c->rank * wpr;
-  uint8_t* codes = d_codes_all ? d_codes_all + c->rank * wpr * 64 : nullptr;
-  if (!codes) {
-    if (c->comm_codes.ensure(std::max<uint64_t>(m, 1))) return CESS_BLS_E_OOM;
-    codes = c->comm_codes.as<uint8_t>();
-  }
-  // words of the rank's run past its last record (a short or empty last shard)
+  uint8_t* codes = d_codes_all ? d_codes_all + c->rank * wpr * 64 : c->comm_codes.as<uint8_t>();
+  // (2) the shard's pipeline; words of the rank's run past its last record (a
+  // short or empty last shard) are zero
   const uint64_t used = (m + 63) / 64;
-  if (used < wpr) HIPCHK(hipMemsetAsync(my_words + used, 0, (wpr - used) * 8, s));
-  for (uint64_t off = 0; off < m; off += c->cap) {
+  if (!r && used < wpr && hipMemsetAsync(my_words + used, 0, (wpr - used) * 8, s) != hipSuccess) r = CESS_BLS_E_HIP;
+  for (uint64_t off = 0; !r && off < m; off += c->cap) {
     const uint64_t q = std::min<uint64_t>(c->cap, m - off);
     r = run_chunk(c, s, q, d_sigs + 48 * off, d_pks + 96 * off, d_msgs, d_offs + off, nullptr, codes + off,
                   my_words + off / 64, nullptr);
-    if (r) return r;
-    if (c->flags & CESS_BLS_F_PROFILE) {
-      r = collect_profile(c, s);
-      if (r) return r;
-    }
+    if (!r && (c->flags & CESS_BLS_F_PROFILE)) r = collect_profile(c, s);
   }
-  r = allgather_inplace(c, d_bitmap_all, wpr, ncclUint64, 8, s);
-  if (r) return r;
+  if (r) {
+    // past the agreement the peers are committed to the all-gathers: take part
+    // with a rejecting block (no verdict bit set) and report the failure here
+    (void)hipMemsetAsync(my_words, 0, wpr * 8, s);
+  }
+  // (4)
+  int g = t.allgather_dev(c->device, d_bitmap_all, wpr * 8, s);
   if (d_codes_all) {
-    r = allgather_inplace(c, d_codes_all, wpr * 64, ncclUint8, 1, s);
-    if (r) return r;
+    const int g2 = t.allgather_dev(c->device, d_codes_all, wpr * 64, s);
+    if (!g) g = g2;
   }
+  if (r) return r;
+  if (g) return g;
   return order_end(c, s);
 }
 
@@ -163,28 +257,22 @@ extern "C" int cess_bls_verify_batch_rlc_sharded(cess_bls_ctx* c, size_t n, cons
                                                  uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4,
                                                  int* global_ok_out) {
   ENTRY(c);
-  if (!c->comm) return CESS_BLS_E_NO_COMM;
-  uint8_t gt[576];
-  int r = rlc_begin(c, n, sigs, pks, msgs, offs, seed32, gt);
+  if (!c->xport) return CESS_BLS_E_NO_COMM;
+  Transport& t = *c->xport;
+  // (2) this rank's combination (its shard; scalars distinct across ranks)
+  std::vector<uint8_t> gts((size_t)c->nranks * 576, 0);
+  int st = rlc_begin(c, n, sigs, pks, msgs, offs, seed32, &gts[(size_t)c->rank * 576]);
+  // (3), then the Gt partials: one 576-byte block per rank, multiplied on the
+  // device (RCCL has no Fp12 reduction operator)
+  int r = agree(t, st);
   if (r) return r;
-  // Gt partials: one 576-byte slot per rank, all-gathered in place, multiplied
-  // on the device (RCCL has no Fp12 reduction operator)
-  HIPCHK(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  r = order_begin(c, s);
-  if (r) return r;
-  if (c->comm_buf.ensure((size_t)c->nranks * 576)) return CESS_BLS_E_OOM;
-  uint8_t* d = c->comm_buf.as<uint8_t>();
-  HIPCHK(hipMemcpyAsync(d + (size_t)c->rank * 576, gt, 576, hipMemcpyHostToDevice, s));
-  r = allgather_inplace(c, d, 576, ncclUint8, 1, s);
-  if (r) return r;
-  HIPCHK(hipStreamSynchronize(s));
-  r = order_end(c, s);
+  r = t.allgather_host(gts.data(), 576);
   if (r) return r;
   int one = 0;
-  r = gt_product_is_one(c, c->nranks, d, true, &one);
+  r = gt_product_is_one(c, c->nranks, gts.data(), false, &one);
   if (r) return r;
   if (global_ok_out) *global_ok_out = one;
+  // bisection is shard-local: a rank bisects iff its own check failed
   return rlc_finish(c, codes_out, bitmap_out, stats4);
 }
 
@@ -195,19 +283,14 @@ extern "C" int cess_bls_comm_barrier(cess_bls_ctx* c) {
 
 extern "C" int cess_bls_comm_max_f64(cess_bls_ctx* c, double* value) {
   ENTRY(c);
-  if (!c->comm) return CESS_BLS_E_NO_COMM;
-  if (!value) return CESS_BLS_E_INVALID_ARG;
-  HIPCHK(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  int r = order_begin(c, s);
+  if (!c->xport) return CESS_BLS_E_NO_COMM;
+  // a NULL value still takes part (the collective must not depend on it)
+  double v = value ? *value : 0.0;
+  const int r = c->xport->max_f64(&v);
   if (r) return r;
-  if (c->comm_buf.ensure(std::max<size_t>(8, (size_t)c->nranks * 576))) return CESS_BLS_E_OOM;
-  double* d = c->comm_buf.as<double>();
-  HIPCHK(hipMemcpyAsync(d, value, 8, hipMemcpyHostToDevice, s));
-  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, c->comm, s));
-  HIPCHK(hipMemcpyAsync(value, d, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return order_end(c, s);
+  if (!value) return CESS_BLS_E_INVALID_ARG;
+  *value = v;
+  return CESS_BLS_OK;
 }
 
 // ---------------------------------------------------------------------------

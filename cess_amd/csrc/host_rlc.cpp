@@ -146,6 +146,7 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 // r_i is shared across shards under one seed)
 int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
                         const uint64_t* offs, const uint8_t* seed_in, uint64_t index_hi, uint8_t* gt_out) {
+  if (c->rlc) c->rlc->valid = false;   // whatever happens below, the previous batch is gone
   if (n && (!sigs || !pks || !offs || (!msgs && offs[n] != offs[0]))) return CESS_BLS_E_INVALID_ARG;
   if (n >= (1ull << 32)) return CESS_BLS_E_INVALID_ARG;
   uint8_t seed32[32];
@@ -157,7 +158,8 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   R.n = n, R.sigs = sigs, R.pks = pks, R.msgs = msgs, R.offs = offs;
   R.checks = R.leaves = R.leaf_sigs = 0;
   R.codes.assign(n, 0);
-  R.local_ok = true;
+  R.local_ok = false;
+  R.valid = false;
   R.per_sig = false;
   R.K = 0;
   auto gt_one = [&]() {
@@ -168,6 +170,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   };
   if (n == 0) {
     gt_one();
+    R.local_ok = R.valid = true;
     return CESS_BLS_OK;
   }
   hipStream_t s = c->stream;
@@ -224,6 +227,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     if (r) return r;
     R.leaf_sigs = n;
     gt_one();
+    R.valid = true;
     return CESS_BLS_OK;
   }
   R.gbeg.assign(K + 1, 0);
@@ -320,12 +324,15 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   r = rlc_check_multi(c, R, {{0, n}}, ok, gt_out);
   if (r) return r;
   R.local_ok = ok[0] != 0;
-  return order_end(c, s);
+  r = order_end(c, s);
+  if (r) return r;
+  R.valid = true;
+  return CESS_BLS_OK;
 }
 
 int cess_host::rlc_begin(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
                          const uint64_t* offs, const uint8_t* seed32, uint8_t* gt_out) {
-  const uint64_t hi = c->comm ? ((uint64_t)c->rank << 40) : 0;
+  const uint64_t hi = c->xport ? ((uint64_t)c->rank << 40) : 0;
   return rlc_begin_at(c, n, sigs, pks, msgs, offs, seed32, hi, gt_out);
 }
 
@@ -359,8 +366,9 @@ int cess_host::gt_product_is_one(cess_bls_ctx* c, size_t m, const uint8_t* gts, 
 // one to the shard's partial, so a failed local check proves an invalid member,
 // and no other shard's partial may cancel that proof.
 int cess_host::rlc_finish(cess_bls_ctx* c, uint8_t* codes_out, uint64_t* bitmap_out, uint64_t* stats4) {
-  if (!c->rlc) return CESS_BLS_E_INVALID_ARG;
+  if (!c->rlc || !c->rlc->valid) return CESS_BLS_E_INVALID_ARG;
   RlcState& R = *c->rlc;
+  R.valid = false;   // one finish per begin; a failure below leaves nothing to finish
   const uint64_t n = R.n;
   std::vector<uint8_t>& codes = R.codes;
   if (!R.per_sig && !R.local_ok) {

@@ -45,7 +45,9 @@ extern "C" {
 #define CESS_BLS_E_BUSY (-6)     /* another host thread is inside a call on this context */
 #define CESS_BLS_E_BAD_KEY (-7)  /* cess_bls_enclave_verify_bls: the key does not deserialize (the reference panics) */
 #define CESS_BLS_E_BAD_SIG (-8)  /* cess_bls_enclave_verify_bls: the signature does not deserialize (the reference panics) */
-#define CESS_BLS_E_NO_COMM (-9)  /* a sharded entry point on a context without cess_bls_comm_init */
+#define CESS_BLS_E_NO_COMM (-9)  /* a sharded entry point on a context without cess_bls_comm_init[_shm] */
+/* (-10 is CESS_RSA_E_UNSUPPORTED, include/cess_rsa.h) */
+#define CESS_BLS_E_COMM (-11)    /* shared-memory communicator: a peer timed out or the transport failed */
 
 enum cess_bls_code {
   CESS_BLS_CODE_OK = 0,
@@ -61,6 +63,7 @@ enum cess_bls_code {
 #define CESS_BLS_SK_BYTES 32   /* PrivateKey::BYTES src/lib.rs:178 */
 #define CESS_BLS_GT_BYTES 576
 #define CESS_BLS_COMM_ID_BYTES 128  /* ncclUniqueId */
+#define CESS_BLS_COMM_NAME_BYTES 64  /* cess_bls_comm_shm_name */
 
 typedef struct cess_bls_ctx cess_bls_ctx;
 
@@ -199,12 +202,24 @@ int cess_bls_gt_product_is_one(cess_bls_ctx* ctx, size_t m, const uint8_t* gts, 
 int cess_bls_rlc_finish(cess_bls_ctx* ctx, int global_ok, uint8_t* codes_out, uint64_t* bitmap_out,
                         uint64_t* stats4);
 
-/* ---- multi-GPU: RCCL communicator in the context ----
+/* ---- multi-GPU: communicator in the context ----
  * One process and one context per GPU.  Signatures are independent
  * (src/lib.rs:243 is per signature), so a batch shards by index with no
- * exchange during compute; the only collectives are RCCL all-gathers (over
- * xGMI on one node) of the verdict-bitmap words, optionally of the code bytes,
- * and in RLC mode of the 576-byte Gt partials. */
+ * exchange during compute; the only collectives are all-gathers of the
+ * verdict-bitmap words, of the code bytes, and in RLC mode of the 576-byte Gt
+ * partials, plus a status agreement.
+ *
+ * Transports: RCCL over xGMI (cess_bls_comm_init; production) or host shared
+ * memory (cess_bls_comm_init_shm; processes of one host, which may share one
+ * GPU -- RCCL refuses two ranks on one device -- used to run the shard/merge
+ * code with several ranks on a one-GPU box).  The sharded entry points behave
+ * identically over either.
+ *
+ * Collective contract: every rank calls the same sharded entry points in the
+ * same order.  Each call first agrees on the batch size and, after its local
+ * work, on a status: when any rank fails (bad arguments, HIP error, OOM), EVERY
+ * rank returns that failure (the most negative status) and no verdict data
+ * moves, so one rank's error never leaves the others blocked in a collective. */
 
 /* ncclGetUniqueId on one rank (e.g. rank 0); the caller distributes the 128
  * bytes to every rank out of band. */
@@ -248,6 +263,34 @@ int cess_bls_verify_batch_rlc_sharded(cess_bls_ctx* ctx, size_t n_shard, const u
 /* Control-plane helpers over the same communicator (collective). */
 int cess_bls_comm_barrier(cess_bls_ctx* ctx);
 int cess_bls_comm_max_f64(cess_bls_ctx* ctx, double* value);
+/* "rccl", "shm" or "none" (static string). */
+const char* cess_bls_comm_kind(cess_bls_ctx* ctx);
+
+/* ---- host shared-memory transport ----
+ * A fresh job name (POSIX shm name, NUL-terminated); create it on one rank and
+ * distribute it out of band, like the RCCL id. */
+int cess_bls_comm_shm_name(char name_out[CESS_BLS_COMM_NAME_BYTES]);
+/* Attach the shared-memory transport to the context (collective: every rank
+ * calls it with the same name; returns once all nranks are attached).  Waits
+ * are bounded by env CESS_BLS_COMM_TIMEOUT_MS (default 300000): a rank that
+ * times out fails with CESS_BLS_E_COMM and makes its peers fail too. */
+int cess_bls_comm_init_shm(cess_bls_ctx* ctx, int nranks, int rank, const char* name);
+
+/* Context-free communicator (no device needed): the merge step of the
+ * sharded entry points for callers that verify their shards by other means
+ * (e.g. keyed or device batches per rank), and for tests of the merge on
+ * hosts without a GPU. */
+typedef struct cess_bls_comm cess_bls_comm;
+int cess_bls_comm_open_shm(const char* name, int nranks, int rank, cess_bls_comm** out);
+void cess_bls_comm_close(cess_bls_comm* comm);
+/* *agreed_out = the most negative status passed by any rank (0 if none failed). */
+int cess_bls_comm_agree(cess_bls_comm* comm, int status, int* agreed_out);
+/* shard_codes: this rank's shard (cess_bls_shard_range) of an n_total-record
+ * batch; every rank receives the codes (n_total bytes, may be NULL) and the
+ * bitmap (ceil(n_total/64) words, may be NULL) of the whole batch.  n_total
+ * must be equal on every rank (else CESS_BLS_E_INVALID_ARG on all ranks). */
+int cess_bls_comm_gather_verdicts(cess_bls_comm* comm, uint64_t n_total, const uint8_t* shard_codes,
+                                  uint8_t* codes_out, uint64_t* bitmap_out);
 
 /* ---- device memory on the context's GPU (for callers without a HIP runtime
  * of their own: keep a batch resident in HBM across device-resident calls) */

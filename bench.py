@@ -630,7 +630,9 @@ def main():
         if args.mode == "persig":
             wl = (f"BASELINE config[1]: {n} independent sigs, distinct keys, per-sig 2-pairing verify" if world == 1
                   else f"BASELINE config[2] shape: {n_total} sigs ({n} per GPU) sharded by index across {world} GPUs, "
-                       f"distinct keys, per-sig 2-pairing verify, RCCL all-gather of verdict bitmap + codes")
+                       f"distinct keys, per-sig 2-pairing verify, "
+                       f"{'RCCL' if ctx.comm_kind == 'rccl' else 'shared-memory'} all-gather of verdict bitmap + codes"
+                       + (" (REHEARSAL: all ranks share GPU 0)" if args.one_device else ""))
         elif keyed:
             wl = (f"BASELINE config[3] shape, per-signature verdicts: {n} sigs per GPU over {args.keys} keys, key "
                   f"decode + G2Prepared once per key (keyed batch)")

@@ -1,8 +1,8 @@
 # Round check on one MI355X box: -m gpu tests, smoke, the N=1 bench, and a
 # rehearsal of the N=2 sharded path (two ranks on GPU 0 over the shared-memory
-# transport; its throughput is not an N-GPU figure).  Usage: TAG=r04a bash tools/gpu_check.sh
+# transport; its throughput is not an N-GPU figure).  Usage: TAG=round3_x bash tools/gpu_check.sh
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-T=${TAG:-r04a}
+T=${TAG:-round3}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.txt 2>&1
 rc=$?; tail -5 gpurun_out/${T}_pytest.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.txt 2>&1 || exit 3

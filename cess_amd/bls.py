@@ -48,6 +48,9 @@ EXPORTS = (
     # transport seam of the sharded entry points (RCCL or host shared memory)
     "cess_bls_comm_kind", "cess_bls_comm_shm_name", "cess_bls_comm_init_shm", "cess_bls_comm_open_shm",
     "cess_bls_comm_close", "cess_bls_comm_agree", "cess_bls_comm_gather_verdicts",
+    # node-side services: decode-only batches, the bounded verdict cache
+    "cess_bls_deserialize_batch", "cess_bls_cache_create", "cess_bls_cache_destroy", "cess_bls_cache_clear",
+    "cess_bls_cache_size", "cess_bls_cache_verify_var", "cess_bls_cache_insert_var", "cess_bls_sha256",
     # include/cess_rsa.h (RSA PKCS#1 v1.5 raw verify, cp_enclave_verify::verify_rsa)
     "cess_rsa_parse_key", "cess_rsa_keys_load", "cess_rsa_verify_batch", "cess_rsa_verify_batch_device",
     "cess_rsa_verify",
@@ -59,6 +62,8 @@ RSA_CODE_NAMES = {0: "OK", 1: "SIG_LEN", 2: "SIG_RANGE", 3: "MSG_LEN", 4: "MISMA
 # infrastructure status codes (include/cess_bls.h)
 E_INVALID_ARG, E_NO_DEVICE, E_HIP, E_OOM, E_RCCL, E_BUSY, E_BAD_KEY, E_BAD_SIG, E_NO_COMM = range(-1, -10, -1)
 E_COMM = -11
+KIND_SIG, KIND_PK = 0, 1
+CODE_UNAVAILABLE = 0xFF
 F_PROFILE, F_STRICT_IDENTITY = 1, 2
 MODE_PER_SIG, MODE_RLC = 0, 1
 
@@ -130,6 +135,16 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_comm_close.restype = None
         lib.cess_bls_comm_agree.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         lib.cess_bls_comm_gather_verdicts.argtypes = [vp, ctypes.c_uint64, _u8p, _u8p, _u64p]
+        lib.cess_bls_deserialize_batch.argtypes = [vp, ctypes.c_int, sz, _u8p, _u64p, _u8p]
+        lib.cess_bls_cache_create.argtypes = [sz, ctypes.POINTER(vp)]
+        lib.cess_bls_cache_destroy.argtypes = [vp]
+        lib.cess_bls_cache_destroy.restype = None
+        lib.cess_bls_cache_clear.argtypes = [vp]
+        lib.cess_bls_cache_size.argtypes = [vp]
+        lib.cess_bls_cache_size.restype = ctypes.c_size_t
+        lib.cess_bls_cache_verify_var.argtypes = [vp, vp, sz, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p]
+        lib.cess_bls_cache_insert_var.argtypes = [vp, sz, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p, _u8p]
+        lib.cess_bls_sha256.argtypes = [_u8p, sz, _u8p]
         lib.cess_bls_comm_barrier.argtypes = [vp]
         lib.cess_bls_comm_max_f64.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         lib.cess_bls_device_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
@@ -423,6 +438,17 @@ class Context:
         self._chk(self._lib.cess_bls_comm_max_f64(self._h, ctypes.byref(d)))
         return d.value
 
+    # --- deserialize only (Signature/PublicKey::deserialize, no pairing) ---
+    def deserialize_codes(self, kind: int, encodings: Sequence[bytes]) -> bytes:
+        """Per-encoding codes: 0 or SIG_LEN/SIG_POINT (kind KIND_SIG), PK_LEN/PK_POINT (KIND_PK)."""
+        n = len(encodings)
+        if n == 0:
+            return b""
+        codes = (ctypes.c_uint8 * n)()
+        self._chk(self._lib.cess_bls_deserialize_batch(self._h, kind, n, _buf(b"".join(bytes(e) for e in encodings)),
+                                                       _offsets([len(e) for e in encodings]), codes))
+        return bytes(codes)
+
     # --- device memory on this context's GPU -------------------------------
     def device_alloc(self, nbytes: int) -> int:
         p = ctypes.c_void_p()
@@ -638,6 +664,71 @@ class Comm:
         return bytes(codes)[:n_total], list(bitmap)[: (n_total + 63) // 64]
 
 
+def sha256(data: bytes) -> bytes:
+    """The library's host SHA-256 (the verdict cache's key derivation)."""
+    lib = load_library()
+    out = (ctypes.c_uint8 * 32)()
+    data = bytes(data)
+    st = lib.cess_bls_sha256(_buf(data), len(data), out)
+    if st != 0:
+        raise BlsInfraError(lib.cess_bls_status_string(st).decode(), st)
+    return bytes(out)
+
+
+class VerdictCache:
+    """Bounded verdict cache (cess_bls_cache_*): what the node host function
+    reads and the node batcher fills.  Needs no GPU for lookups and inserts."""
+
+    def __init__(self, capacity: int):
+        self._lib = load_library()
+        h = ctypes.c_void_p()
+        st = self._lib.cess_bls_cache_create(capacity, ctypes.byref(h))
+        if st != 0:
+            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode(), st)
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.cess_bls_cache_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(self._lib.cess_bls_cache_size(self._h))
+
+    def clear(self):
+        self._lib.cess_bls_cache_clear(self._h)
+
+    @staticmethod
+    def _flat(records):
+        sigs = [bytes(r[0]) for r in records]
+        msgs = [bytes(r[1]) for r in records]
+        keys = [bytes(r[2]) for r in records]
+        return (_buf(b"".join(sigs)), _offsets([len(x) for x in sigs]), _buf(b"".join(keys)),
+                _offsets([len(x) for x in keys]), _buf(b"".join(msgs)), _offsets([len(x) for x in msgs]))
+
+    def verify(self, records, ctx: Optional[Context] = None):
+        """(status, codes, stats) for (sig, msg, key) records: hits from the cache,
+        misses verified in one batch on ctx (None: reported CODE_UNAVAILABLE)."""
+        n = len(records)
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        st3 = (ctypes.c_uint64 * 3)()
+        st = self._lib.cess_bls_cache_verify_var(self._h, ctx.handle if ctx is not None else None, n,
+                                                 *self._flat(records), codes, st3)
+        return st, bytes(codes)[:n], {"hits": st3[0], "verified": st3[1], "evicted": st3[2]}
+
+    def insert(self, records, codes: bytes):
+        n = len(records)
+        st = self._lib.cess_bls_cache_insert_var(self._h, n, *self._flat(records), _buf(bytes(codes)))
+        if st != 0:
+            raise BlsInfraError(self._lib.cess_bls_status_string(st).decode(), st)
+
+
 def default_context() -> Context:
     global _default
     if _default is None:
@@ -706,7 +797,7 @@ class PublicKey:
         b = bytes(b)
         if len(b) != cls.BYTES:
             raise DeserializeError(InvalidPublicKey.WrongLength)
-        code = default_context().verify_codes([(_ID_SIG, b"", b)])[0]
+        code = default_context().deserialize_codes(KIND_PK, [b])[0]      # decode kernels only
         if code == CODE_PK_POINT:
             raise DeserializeError(InvalidPublicKey.InvalidPoint)
         return cls(b)
@@ -736,7 +827,7 @@ class Signature:
         b = bytes(b)
         if len(b) != cls.BYTES:
             raise DeserializeError(InvalidSignature.WrongLength)
-        code = default_context().verify_codes([(b, b"", _ID_PK)])[0]
+        code = default_context().deserialize_codes(KIND_SIG, [b])[0]     # decode kernels only
         if code == CODE_SIG_POINT:
             raise DeserializeError(InvalidSignature.InvalidPoint)
         return cls(b)

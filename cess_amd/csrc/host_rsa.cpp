@@ -72,13 +72,24 @@ bool parse_pkcs1(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t
   if (eb.size() > 8) return false;
   e = 0;
   for (uint8_t v : eb) e = (e << 8) | v;
-  // rsa 0.8 key checks: n at most 4096 bits (odd, > 2), 2 <= e <= 2^33 - 1
-  if (mod.empty() || mod.size() > 512 || !(mod.back() & 1) || (mod.size() == 1 && mod[0] < 3)) return false;
+  // rsa 0.8 key checks (RsaPublicKey::new -> check_public): n at most 4096
+  // bits, 2 <= e <= 2^33 - 1.  Keys the crate accepts but this verifier cannot
+  // represent (even or tiny moduli) are reported by kernel_can_verify, not here.
+  if (mod.empty() || mod.size() > 512) return false;
   if (e < 2 || e > (1ull << 33) - 1) return false;
   return true;
 }
 
-bool parse_spki(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t& e) {
+// Montgomery arithmetic needs an odd modulus > 2: other moduli that parse are
+// CESS_RSA_E_UNSUPPORTED (the caller's CPU path decides), never BAD_KEY, so a
+// GPU node cannot turn a key the rsa crate accepts into a rejection
+bool kernel_can_verify(const std::vector<uint8_t>& mod) {
+  return (mod.back() & 1) && !(mod.size() == 1 && mod[0] < 3);
+}
+
+// *unsup: the AlgorithmIdentifier carries parameters other than NULL (the
+// crate's acceptance of those is unpinned here: reported as unsupported)
+bool parse_spki(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t& e, bool* unsup) {
   Tlv seq, alg, bits, oid, nul;
   if (!tlv(b, n, 0, seq) || seq.tag != 0x30 || seq.end != n) return false;
   if (!tlv(seq.v, seq.len, 0, alg) || alg.tag != 0x30) return false;
@@ -87,7 +98,8 @@ bool parse_spki(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t&
       memcmp(oid.v, kRsaOid, sizeof(kRsaOid)) != 0)
     return false;
   if (oid.end != alg.len) {
-    if (!tlv(alg.v, alg.len, oid.end, nul) || nul.tag != 0x05 || nul.len != 0 || nul.end != alg.len) return false;
+    if (!tlv(alg.v, alg.len, oid.end, nul) || nul.end != alg.len) return false;
+    if (nul.tag != 0x05 || nul.len != 0) *unsup = true;
   }
   if (bits.len < 1 || bits.v[0] != 0) return false;
   return parse_pkcs1(bits.v + 1, bits.len - 1, mod, e);
@@ -185,8 +197,11 @@ static int load_table(cess_bls_ctx* c, RsaTable& T, size_t k, const uint8_t* der
     const uint8_t* d = ders + offs[j];
     const size_t len = offs[j + 1] - offs[j];
     int st = CESS_BLS_OK;
-    const bool parsed = format == CESS_RSA_KEY_PKCS1 ? parse_pkcs1(d, len, mod, e) : parse_spki(d, len, mod, e);
+    bool unsup = false;
+    const bool parsed =
+        format == CESS_RSA_KEY_PKCS1 ? parse_pkcs1(d, len, mod, e) : parse_spki(d, len, mod, e, &unsup);
     if (!parsed) st = CESS_BLS_E_BAD_KEY;
+    else if (unsup || !kernel_can_verify(mod)) st = CESS_RSA_E_UNSUPPORTED;
     int L = 0;
     if (st == CESS_BLS_OK) {
       size_t bits = 8 * mod.size();
@@ -282,7 +297,8 @@ extern "C" int cess_rsa_parse_key(const uint8_t* der, size_t len, int format, ui
   if ((!der && len) || !n_len || !e_out) return CESS_BLS_E_INVALID_ARG;
   std::vector<uint8_t> mod;
   uint64_t e = 0;
-  const bool ok = format == CESS_RSA_KEY_PKCS1 ? parse_pkcs1(der, len, mod, e) : parse_spki(der, len, mod, e);
+  bool unsup = false;
+  const bool ok = format == CESS_RSA_KEY_PKCS1 ? parse_pkcs1(der, len, mod, e) : parse_spki(der, len, mod, e, &unsup);
   if (!ok) return CESS_BLS_E_BAD_KEY;
   *n_len = mod.size();
   *e_out = e;

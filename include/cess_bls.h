@@ -309,6 +309,50 @@ int cess_bls_synchronize(cess_bls_ctx* ctx);
 int cess_bls_enclave_verify_bls(cess_bls_ctx* ctx, const uint8_t* key, size_t key_len, const uint8_t* msg,
                                 size_t msg_len, const uint8_t* sig, size_t sig_len, int* ok_out);
 
+/* ---- deserialize only (no pairing) ----
+ * Signature::deserialize (src/lib.rs:138-152) for kind CESS_BLS_KIND_SIG, or
+ * PublicKey::deserialize (src/lib.rs:68-82, including the G2 subgroup check)
+ * for CESS_BLS_KIND_PK, over n encodings of any length (record i =
+ * data[offsets[i] .. offsets[i+1])): codes_out[i] = 0, or SIG_LEN / SIG_POINT
+ * (PK_LEN / PK_POINT).  Runs the decode kernels alone, so one call costs a
+ * decode's latency, not a verification's.  Host buffers. */
+#define CESS_BLS_KIND_SIG 0
+#define CESS_BLS_KIND_PK 1
+int cess_bls_deserialize_batch(cess_bls_ctx* ctx, int kind, size_t n, const uint8_t* data, const uint64_t* offsets,
+                               uint8_t* codes_out);
+
+/* ---- verdict cache (node host function + batcher) ----
+ * Thread-safe map from a record -- SHA-256 over the length-prefixed (sig, msg,
+ * key) bytes -- to its verdict code, bounded by `capacity` entries (at
+ * capacity the oldest entries are evicted first, so memory stays bounded
+ * whatever a transaction pool receives).  Only verdicts (codes 0..5) are ever
+ * stored. */
+#define CESS_BLS_CODE_UNAVAILABLE 0xff  /* no verdict: the caller's own path (e.g. the runtime's wasm verifier) decides */
+typedef struct cess_bls_cache cess_bls_cache;
+int cess_bls_cache_create(size_t capacity, cess_bls_cache** out);
+void cess_bls_cache_destroy(cess_bls_cache* cache);
+int cess_bls_cache_clear(cess_bls_cache* cache);
+size_t cess_bls_cache_size(cess_bls_cache* cache);
+/* Codes for n records of any lengths (layout of cess_bls_verify_batch_var):
+ * cached records from the cache; the others (each distinct record once)
+ * verified in ONE batch on ctx and inserted.  ctx NULL, or a batch that fails
+ * (infrastructure): those records get CESS_BLS_CODE_UNAVAILABLE, nothing is
+ * inserted, and the batch's status is returned (CESS_BLS_E_NO_DEVICE for
+ * NULL) -- codes_out is filled in every case.  stats3 (may be NULL): cache
+ * hits, records verified, entries evicted by this call. */
+int cess_bls_cache_verify_var(cess_bls_cache* cache, cess_bls_ctx* ctx, size_t n, const uint8_t* sig_data,
+                              const uint64_t* sig_offsets, const uint8_t* pk_data, const uint64_t* pk_offsets,
+                              const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* codes_out,
+                              uint64_t* stats3);
+/* Insert verdicts obtained elsewhere (e.g. the gathered codes of a sharded
+ * batch); codes must be verdicts (0..5). */
+int cess_bls_cache_insert_var(cess_bls_cache* cache, size_t n, const uint8_t* sig_data, const uint64_t* sig_offsets,
+                              const uint8_t* pk_data, const uint64_t* pk_offsets, const uint8_t* msgs,
+                              const uint64_t* msg_offsets, const uint8_t* codes);
+/* SHA-256 of the cache keys (exposed so callers and tests can check the key
+ * derivation). */
+int cess_bls_sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+
 /* Per-stage timings (ms, summed since the last reset) when CESS_BLS_F_PROFILE is
  * set.  names/ms arrays of length max; returns the number of stages. */
 int cess_bls_stage_times(cess_bls_ctx* ctx, const char** names, double* ms, int max, int reset);

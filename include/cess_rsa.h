@@ -13,9 +13,15 @@
  * 3 MSG_LEN (k < len(msg) + 11), 4 MISMATCH, 5 KEY (no such key / the key did
  * not load).  Codes 1..5 are the reference's `false`.  Moduli of up to 2048
  * bits are verified on the GPU (1024/2048-bit size classes; Podr2Key is a
- * 2048-bit key); the reference also parses 2049..4096-bit keys: those report
- * CESS_RSA_E_UNSUPPORTED at load time.  Return values are infrastructure
- * status as in cess_bls.h.
+ * 2048-bit key).  Keys the reference accepts but the GPU cannot verify --
+ * 2049..4096-bit moduli, even moduli, n < 3, SPKI AlgorithmIdentifier
+ * parameters other than NULL -- report CESS_RSA_E_UNSUPPORTED, never
+ * CESS_BLS_E_BAD_KEY: the verdict path for them is the caller's (the node
+ * hook answers "unavailable" and the runtime's unchanged
+ * cp_enclave_verify::verify_rsa decides), so a GPU node never
+ * turns a key the rsa crate accepts into a rejection.  BAD_KEY means the
+ * crate's from_public_key_der fails too (malformed DER, > 4096 bits, e out of
+ * [2, 2^33 - 1]).  Return values are infrastructure status as in cess_bls.h.
  */
 #ifndef CESS_RSA_H
 #define CESS_RSA_H
@@ -26,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CESS_RSA_E_UNSUPPORTED (-10) /* modulus longer than 2048 bits */
+#define CESS_RSA_E_UNSUPPORTED (-10) /* the key parses (the reference accepts it) but the GPU cannot verify it */
 
 enum cess_rsa_code {
   CESS_RSA_OK = 0,
@@ -40,7 +46,7 @@ enum cess_rsa_code {
 #define CESS_RSA_KEY_SPKI 0  /* SubjectPublicKeyInfo DER: what RsaPublicKey::from_public_key_der parses */
 #define CESS_RSA_KEY_PKCS1 1 /* RSAPublicKey DER: Podr2Key = [u8; 270] (primitives/common/src/lib.rs:54) */
 
-/* Host-side DER parse (the key checks of rsa 0.8: n <= 4096 bits, odd;
+/* Host-side DER parse (the key checks of rsa 0.8: n <= 4096 bits,
  * 2 <= e <= 2^33 - 1).  n_out (may be NULL) receives the big-endian modulus
  * (*n_len bytes).  CESS_BLS_E_BAD_KEY where from_public_key_der fails. */
 int cess_rsa_parse_key(const uint8_t* der, size_t len, int format, uint8_t* n_out, size_t n_cap, size_t* n_len,
@@ -68,7 +74,8 @@ int cess_rsa_verify_batch_device(cess_bls_ctx* ctx, size_t n, const uint32_t* d_
 
 /* cp_enclave_verify::verify_rsa(key, msg, sig) drop-in: SPKI DER key;
  * CESS_BLS_E_BAD_KEY where from_public_key_der(key).unwrap() panics
- * (CESS_RSA_E_UNSUPPORTED for > 2048-bit keys); else *ok_out = the verdict. */
+ * (CESS_RSA_E_UNSUPPORTED for keys the GPU cannot verify, see above); else
+ * *ok_out = the verdict. */
 int cess_rsa_verify(cess_bls_ctx* ctx, const uint8_t* key_der, size_t key_len, const uint8_t* msg, size_t msg_len,
                     const uint8_t* sig, size_t sig_len, int* ok_out);
 

@@ -10,9 +10,13 @@ The arithmetic lives in the third-party crate `rsa` 0.8.2
 and not in this image, so this module restates its published behaviour:
 
 * from_public_key_der: SubjectPublicKeyInfo DER (RFC 5280) with algorithm
-  rsaEncryption (1.2.840.113549.1.1.1, NULL parameters) wrapping an RFC 8017
-  RSAPublicKey SEQUENCE { INTEGER n, INTEGER e }; the key checks of rsa 0.8
-  (n at most 4096 bits, 2 <= e <= 2^33 - 1).  Failure -> the reference panics.
+  rsaEncryption (1.2.840.113549.1.1.1) wrapping an RFC 8017 RSAPublicKey
+  SEQUENCE { INTEGER n, INTEGER e }; the key checks of rsa 0.8
+  (RsaPublicKey::new -> check_public: n at most 4096 bits, 2 <= e <= 2^33 - 1).
+  Failure -> the reference panics.  The crate's check_public has no parity or
+  size-floor check on n and its AlgorithmIdentifier handling asserts the OID
+  only, so even moduli, n = 1 and non-NULL parameters parse here (unpinned:
+  the GPU library reports such keys CESS_RSA_E_UNSUPPORTED, never BAD_KEY).
 * Pkcs1v15Sign::new_raw(): no DigestInfo prefix and no hash-length check, so
   the signed "hashed" value is the message bytes themselves.
 * verify (RFC 8017 RSASSA-PKCS1-v1_5-VERIFY with an empty T prefix):
@@ -97,8 +101,8 @@ def parse_spki(der: bytes):
     if to != 0x06 or oid != RSA_OID:
         raise KeyError_("not rsaEncryption")
     if q != len(alg):
-        tn, nul, q = _tlv(alg, q)
-        if tn != 0x05 or nul or q != len(alg):
+        tn, nul, q = _tlv(alg, q)       # any single parameters element (OID checked only)
+        if q != len(alg):
             raise KeyError_("bad parameters")
     if not bits or bits[0] != 0:
         raise KeyError_("unused bits")
@@ -106,7 +110,7 @@ def parse_spki(der: bytes):
 
 
 def _check(n: int, e: int):
-    if n.bit_length() > MAX_BITS or n < 3 or n % 2 == 0:
+    if n.bit_length() > MAX_BITS or n == 0:
         raise KeyError_("modulus")
     if not MIN_E <= e <= MAX_E:
         raise KeyError_("exponent")

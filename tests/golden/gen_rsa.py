@@ -68,7 +68,6 @@ def main():
                 {"name": "trailing", "der": (good + b"\x00").hex()},
                 {"name": "wrong_oid", "der": good.replace(o.RSA_OID, bytes.fromhex("2a8648ce3d0201")).hex()},
                 {"name": "pkcs1_not_spki", "der": out_keys[0]["pkcs1"]},
-                {"name": "even_modulus", "der": o.encode_spki(keys[0]["n"] + 1, 65537).hex()},
                 {"name": "e_one", "der": o.encode_spki(keys[0]["n"], 1).hex()},
                 {"name": "empty", "der": ""}]
     for b in bad_keys:
@@ -78,6 +77,18 @@ def main():
         except o.KeyError_:
             b["parses"] = False
     assert not any(b["parses"] for b in bad_keys)
+    # keys the rsa crate parses (check_public has no parity check; the SPKI
+    # parameters are not inspected) but Montgomery arithmetic cannot verify:
+    # the GPU library reports CESS_RSA_E_UNSUPPORTED for them, never BAD_KEY
+    alg_params = (b"\x30\x0d\x06\x09" + o.RSA_OID + b"\x05\x00",
+                  b"\x30\x0f\x06\x09" + o.RSA_OID + b"\x04\x02\xab\xcd")
+    unsupported = [{"name": "even_modulus", "der": o.encode_spki(keys[0]["n"] + 1, 65537).hex()},
+                   {"name": "modulus_one", "der": o.encode_spki(1, 65537).hex()},
+                   {"name": "params_not_null", "der": good.replace(alg_params[0], alg_params[1])
+                    .replace(good[:4], good[:3] + bytes([good[3] + 2])).hex()}]
+    for u in unsupported:
+        n_, e_ = o.parse_spki(bytes.fromhex(u["der"]))     # parses (the reference accepts it)
+        u["n_bits"] = n_.bit_length()
     # bench pool (bench.py --mode rsa): valid raw signatures over 32-byte
     # messages under key 0 (2048-bit), replicated by the bench to its batch size
     n0, d0 = keys[0]["n"], keys[0]["d"]
@@ -87,7 +98,8 @@ def main():
         pool.append({"msg": m.hex(), "sig": o.sign_raw(n0, d0, m).hex()})
     doc = {"generator": "tests/golden/gen_rsa.py (oracle/rsa_oracle.py)",
            "codes": {"0": "OK", "1": "SIG_LEN", "2": "SIG_RANGE", "3": "MSG_LEN", "4": "MISMATCH"},
-           "keys": out_keys, "cases": cases, "bad_keys": bad_keys, "bench_pool_key0": pool}
+           "keys": out_keys, "cases": cases, "bad_keys": bad_keys,
+           "unsupported_keys": unsupported, "bench_pool_key0": pool}
     with open(os.path.join(ROOT, "tests", "golden", "rsa_vectors.json"), "w") as f:
         json.dump(doc, f, indent=1)
     print(len(cases), "cases,", len(bad_keys), "bad keys")

@@ -64,6 +64,12 @@ def test_host_der_parser_matches_oracle(rv):
         with pytest.raises(bls.BlsInfraError) as ei:
             bls.rsa_parse_key(bytes.fromhex(b["der"]), bls.RSA_KEY_SPKI)
         assert ei.value.status == bls.E_BAD_KEY, b["name"]
+    # keys the rsa crate accepts but Montgomery arithmetic cannot verify parse
+    # like the oracle (never BAD_KEY where the crate has a verdict)
+    for u in rv["unsupported_keys"]:
+        n, e = o.parse_spki(bytes.fromhex(u["der"]))
+        mod, ee = bls.rsa_parse_key(bytes.fromhex(u["der"]), bls.RSA_KEY_SPKI)
+        assert int.from_bytes(mod, "big") == n and ee == e, u["name"]
 
 
 def _gpu_ctx():
@@ -114,6 +120,14 @@ def test_gpu_verify_rsa_dropin(rv):
             with pytest.raises(bls.BlsInfraError) as ei:
                 c.verify_rsa(bytes.fromhex(b["der"]), b"hello world!", bytes(256))
             assert ei.value.status == bls.E_BAD_KEY
+        # parsed by the reference, not verifiable here: UNSUPPORTED (the caller's
+        # CPU path decides), never BAD_KEY
+        for u in rv["unsupported_keys"]:
+            with pytest.raises(bls.BlsInfraError) as ei:
+                c.verify_rsa(bytes.fromhex(u["der"]), b"hello world!", bytes(256))
+            assert ei.value.status == bls.RSA_E_UNSUPPORTED, u["name"]
+        st = c.rsa_keys_load([bytes.fromhex(u["der"]) for u in rv["unsupported_keys"]])
+        assert st == [bls.RSA_E_UNSUPPORTED] * len(rv["unsupported_keys"])
     finally:
         c.close()
 

@@ -1,0 +1,112 @@
+"""Node-side services of the C ABI: the bounded
+verdict cache behind the node host function / batcher
+(utils/cess-gpu-verify-runtime), and the decode-only deserialize batch behind
+the crate's PublicKey::deserialize / Signature::deserialize
+(utils/verify-bls-signatures/src/lib.rs:68-82, :138-152).
+
+CPU (no GPU needed): the cache key derivation (SHA-256) against hashlib; hit,
+miss, dedup, FIFO eviction and "unavailable" semantics with no context --
+records without a cached verdict are CODE_UNAVAILABLE and nothing is cached,
+so the caller's own path decides.
+GPU: the cache's one-batch verification of the misses equals the golden codes
+(all fixed-length and wrong-length cases), a second call is served from the
+cache, and deserialize codes equal the oracle's decode of every golden encoding.
+"""
+import hashlib
+import random
+
+import pytest
+
+from cess_amd import bls
+
+
+def test_sha256_matches_hashlib():
+    rng = random.Random(3)
+    for n in (0, 1, 55, 56, 63, 64, 65, 119, 120, 1000):
+        d = rng.randbytes(n)
+        assert bls.sha256(d) == hashlib.sha256(d).digest()
+
+
+def _recs(k, seed=1):
+    rng = random.Random(seed)
+    return [(rng.randbytes(48), rng.randbytes(32), rng.randbytes(96)) for _ in range(k)]
+
+
+def test_cache_without_device_reports_unavailable():
+    c = bls.VerdictCache(16)
+    recs = _recs(5)
+    st, codes, stats = c.verify(recs, ctx=None)
+    assert st == bls.E_NO_DEVICE
+    assert codes == bytes([bls.CODE_UNAVAILABLE]) * 5
+    assert len(c) == 0 and stats["hits"] == 0          # nothing invented, nothing cached
+
+
+def test_cache_hits_dedup_and_fifo_eviction():
+    c = bls.VerdictCache(4)
+    recs = _recs(6, seed=2)
+    c.insert(recs[:3], bytes([0, 5, 2]))
+    st, codes, stats = c.verify(recs[:3] + [recs[1]], ctx=None)
+    assert st == 0 and codes == bytes([0, 5, 2, 5]) and stats["hits"] == 4
+    # lengths are part of the key: the same bytes split differently never hit
+    s, m, k = recs[0]
+    st, codes, _ = c.verify([(s + m[:1], m[1:], k)], ctx=None)
+    assert codes == bytes([bls.CODE_UNAVAILABLE])
+    # a miss repeated in one call is one record; still unavailable without a context
+    st, codes, stats = c.verify([recs[4], recs[4], recs[0]], ctx=None)
+    assert st == bls.E_NO_DEVICE and codes == bytes([bls.CODE_UNAVAILABLE] * 2 + [0]) and stats["hits"] == 1
+    # capacity 4: inserting 3 more evicts the oldest two (FIFO), memory stays bounded
+    c.insert(recs[3:6], bytes([0, 0, 4]))
+    assert len(c) == 4
+    _, codes, _ = c.verify(recs, ctx=None)
+    assert codes == bytes([bls.CODE_UNAVAILABLE, bls.CODE_UNAVAILABLE, 2, 0, 0, 4])
+    # refreshing an existing record does not grow the cache
+    c.insert([recs[2]], bytes([2]))
+    assert len(c) == 4
+    with pytest.raises(bls.BlsInfraError):
+        c.insert([recs[0]], bytes([bls.CODE_UNAVAILABLE]))   # only verdicts are stored
+    c.clear()
+    assert len(c) == 0
+
+
+def _golden_records(vectors):
+    cases = vectors["cases"] + vectors["length_cases"]
+    return [(bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])) for c in cases], \
+        bytes(c["code"] for c in cases)
+
+
+@pytest.mark.gpu
+def test_cache_verify_equals_golden(ctx, vectors):
+    recs, expect = _golden_records(vectors)
+    c = bls.VerdictCache(1 << 16)
+    st, codes, stats = c.verify(recs + recs[:5], ctx=ctx)      # duplicates verified once
+    assert st == 0
+    assert codes == expect + expect[:5]
+    assert stats["verified"] == len(set(recs)) and stats["hits"] == 0
+    st, codes, stats = c.verify(recs, ctx=ctx)                  # all served by the cache
+    assert st == 0 and codes == expect and stats["hits"] == len(recs) and stats["verified"] == 0
+
+
+@pytest.mark.gpu
+def test_deserialize_equals_oracle(ctx, vectors):
+    import oracle.bls_oracle as o
+
+    def code_of(fn, b, n, bad_len, bad_point):
+        if len(b) != n:
+            return bad_len
+        try:
+            fn(b)
+            return 0
+        except o.Invalid:
+            return bad_point
+
+    cases = vectors["cases"] + vectors["length_cases"]
+    sigs = [bytes.fromhex(c["sig"]) for c in cases]
+    pks = [bytes.fromhex(c["pk"]) for c in cases]
+    want_s = bytes(code_of(o.g1_from_compressed, s, 48, 1, 2) for s in sigs)
+    want_p = bytes(code_of(o.g2_from_compressed, p, 96, 3, 4) for p in pks)
+    assert set(want_s) >= {0, 1, 2} and set(want_p) >= {0, 3, 4}
+    assert ctx.deserialize_codes(bls.KIND_SIG, sigs) == want_s
+    assert ctx.deserialize_codes(bls.KIND_PK, pks) == want_p
+    # the reference-API mirror now takes the decode-only path
+    ok_pk = next(p for p, w in zip(pks, want_p) if w == 0)
+    assert bls.PublicKey.deserialize(ok_pk).serialize() == ok_pk

@@ -1,7 +1,8 @@
-// UNCOMPILED SKETCH (no cargo here): what node/src adds to route the
-// gpu_verify host functions (../src/lib.rs) to an MI355X.  Replaces nothing:
-// the reference executor exposes only the benchmarking host functions
-// (node/src/executor.rs:8).
+// UNCOMPILED (no cargo here) -- what node/src adds to route the gpu_verify
+// host functions (../src/lib.rs) to an MI355X.  Replaces nothing: the
+// reference executor exposes only the benchmarking host functions
+// (node/src/executor.rs:8).  The batcher task is patches/node_batcher.rs
+// (node/src/gpu_batcher.rs).
 
 // --- node/src/executor.rs ---------------------------------------------------
 impl sc_executor::NativeExecutionDispatch for ExecutorDispatch {
@@ -31,9 +32,11 @@ impl sc_client_api::execution_extensions::ExtensionsFactory<Block> for GpuExtens
     }
 }
 
-// in new_partial(), after the client is built:
-//     let gpu = cess_gpu_verify_runtime::ext::GpuState::new(&verify_bls_signatures_gpu::Config {
-//         device: config.gpu_device.unwrap_or(0), max_batch: 1 << 20, ..Default::default() });
-//     client.execution_extensions().set_extensions_factory(GpuExtensionsFactory(gpu.clone()));
-//     task_manager.spawn_handle().spawn("gpu-verify-batcher", None,
-//         crate::gpu_batcher::run(transaction_pool.clone(), gpu));   // patches/node_batcher.rs
+// in new_partial(), after the client is built (no GPU: GpuState still comes
+// up, every host call answers UNAVAILABLE and the runtime's wasm path runs):
+//     if let Some(gpu) = cess_gpu_verify_runtime::ext::GpuState::new(&verify_bls_signatures_gpu::Config {
+//         device: config.gpu_device.unwrap_or(0), max_batch: 1 << 20, ..Default::default() }) {
+//         client.execution_extensions().set_extensions_factory(GpuExtensionsFactory(gpu.clone()));
+//         task_manager.spawn_handle().spawn("gpu-verify-batcher", None,
+//             crate::gpu_batcher::run(transaction_pool.clone(), client.clone(), gpu));
+//     }

@@ -2,48 +2,92 @@
 //!: the `sp_runtime_interface` the reference left
 //! commented out at primitives/enclave-verify/src/lib.rs:10-14 and :35-44,
 //! backed natively by the C ABI (include/cess_bls.h, include/cess_rsa.h)
-//! through the `verify-bls-signatures-gpu` crate.
+//! through the `ic-verify-bls-signature-gpu` crate.
 //!
 //! UNCOMPILED HERE: this image has no cargo/rustc.  It is written against the
 //! substrate crates the reference pins (Cargo.lock: sp-runtime-interface 7,
-//! sp-externalities 0.13) and the C ABI this repository builds and tests.
+//! sp-externalities 0.13, sp-api 4.0.0-dev) and the C ABI this repository
+//! builds and tests.  The behaviour the host functions rely on -- the verdict
+//! cache, its one-batch verification of misses and its "unavailable" answer --
+//! is the C library's `cess_bls_cache_*`, tested through ctypes against the
+//! golden codes (tests/test_service.py, CPU and MI355X).
 //!
-//! Consensus: a host function's result must not depend on the node's
-//! hardware.  The GPU verdicts are bit-exact with the reference crate
-//! (tests/test_gpu_parity.py, golden fixtures pinned by the reference KATs),
-//! every infrastructure failure falls back to the reference crate on the CPU,
-//! and a node without the extension registered runs the CPU path -- so every
-//! node returns the same verdicts.
+//! Consensus: a host function's answer must not depend on the node's hardware.
+//! The host functions therefore carry NO verifier of their own besides the
+//! GPU: every answer is either a GPU verdict (bit-exact with the reference
+//! crate: tests/test_gpu_parity.py, fixtures pinned by the reference KATs) or
+//! `UNAVAILABLE` (no extension, no device, an infrastructure failure, a key the
+//! GPU cannot represent), on which the runtime runs its own, unchanged
+//! `cp_enclave_verify` code (`runtime::verify_bls` / `runtime::verify_rsa`
+//! below).  So every node reaches the reference's verdict, and a node without a
+//! GPU simply executes the original wasm path.
 #![cfg_attr(not(feature = "std"), no_std)]
 
 use sp_runtime_interface::runtime_interface;
 use sp_std::vec::Vec;
 
+/// Answers of the single-record host functions.
+pub const HOOK_FALSE: u8 = 0;
+pub const HOOK_TRUE: u8 = 1;
+/// No GPU verdict: the runtime's own verifier decides (and panics where the
+/// reference panics -- a key or signature that does not deserialize).
+pub const HOOK_UNAVAILABLE: u8 = 0xff;
+
 /// Verdict codes of `verify_bls_batch` (include/cess_bls.h): 0 OK, 1 SIG_LEN,
-/// 2 SIG_POINT, 3 PK_LEN, 4 PK_POINT, 5 PAIRING_FAIL.
+/// 2 SIG_POINT, 3 PK_LEN, 4 PK_POINT, 5 PAIRING_FAIL, 0xff UNAVAILABLE.
 pub const BLS_OK: u8 = 0;
+pub const BLS_PAIRING_FAIL: u8 = 5;
+pub const BLS_UNAVAILABLE: u8 = 0xff;
 
 #[cfg(feature = "std")]
 pub mod ext {
     //! The externalities extension a node registers to route the host
-    //! functions to a GPU (node/src/service.rs, patches/node_service.rs).
+    //! functions to a GPU (patches/node.rs: node/src/executor.rs and
+    //! node/src/service.rs).
     use parking_lot::Mutex;
-    use std::collections::HashMap;
     use std::sync::Arc;
-    use verify_bls_signatures_gpu::{Config, Verifier};
+    use verify_bls_signatures_gpu::{Config, Error, VerdictCache, Verifier};
 
-    /// Shared GPU verifier plus a verdict cache that the node-side batcher
-    /// (patches/node_batcher.rs) fills ahead of block execution: the runtime's
-    /// per-extrinsic call then costs a hash lookup.
+    /// Entries of the verdict cache: at ~100 B each, 1 M entries bound the
+    /// cache to ~100 MB whatever the transaction pool receives.
+    pub const CACHE_CAPACITY: usize = 1 << 20;
+
+    /// The node's GPU verifier and the C library's bounded verdict cache,
+    /// which the node-side batcher (patches/node_batcher.rs) fills ahead of
+    /// block execution: the runtime's per-extrinsic call is then a lookup.
     pub struct GpuState {
         pub verifier: Mutex<Option<Verifier>>,
-        pub cache: Mutex<HashMap<[u8; 32], u8>>,
+        pub cache: VerdictCache,
     }
 
     impl GpuState {
-        pub fn new(cfg: &Config) -> Arc<Self> {
-            // no GPU / no library: the extension still works, on the CPU path
-            Arc::new(GpuState { verifier: Mutex::new(Verifier::new(cfg).ok()), cache: Mutex::new(HashMap::new()) })
+        /// `None` if the cache cannot be created; a missing GPU is not an
+        /// error (every lookup miss is then UNAVAILABLE: the runtime decides).
+        pub fn new(cfg: &Config) -> Option<Arc<Self>> {
+            let cache = VerdictCache::new(CACHE_CAPACITY).ok()?;
+            Some(Arc::new(GpuState { verifier: Mutex::new(Verifier::new(cfg).ok()), cache }))
+        }
+
+        /// Codes for a batch of records: cached verdicts, the misses verified
+        /// in one GPU batch (cess_bls_cache_verify_var) and cached; without a
+        /// verifier, or when the batch fails, the misses are BLS_UNAVAILABLE
+        /// and nothing is cached.
+        pub fn batch_codes(&self, recs: &[(&[u8], &[u8], &[u8])]) -> Vec<u8> {
+            let mut guard = self.verifier.lock();
+            let (codes, _stats, _status) = self.cache.verify(guard.as_mut(), recs);
+            codes
+        }
+
+        /// `cp_enclave_verify::verify_rsa` on the GPU: Some(verdict), or None
+        /// (no device, infrastructure failure, a key the reference parses but
+        /// the GPU cannot verify, a key that does not parse -- the runtime's
+        /// own call then reproduces the reference, panic included).
+        pub fn rsa(&self, key: &[u8], msg: &[u8], sig: &[u8]) -> Option<bool> {
+            let mut guard = self.verifier.lock();
+            match guard.as_mut()?.verify_rsa(key, msg, sig) {
+                Ok(v) => Some(v),
+                Err(Error::BadKey) | Err(Error::Unsupported) | Err(_) => None,
+            }
         }
     }
 
@@ -51,110 +95,87 @@ pub mod ext {
         /// Registered by the node; absent in wasm-only execution and tests.
         pub struct GpuVerifierExt(Arc<GpuState>);
     }
-
-    /// Cache key of one record: blake2-256 over (sig, msg, key) with lengths.
-    pub fn record_key(sig: &[u8], msg: &[u8], key: &[u8]) -> [u8; 32] {
-        let mut buf = Vec::with_capacity(24 + sig.len() + msg.len() + key.len());
-        for part in [sig, msg, key] {
-            buf.extend_from_slice(&(part.len() as u64).to_le_bytes());
-            buf.extend_from_slice(part);
-        }
-        sp_core_hashing::blake2_256(&buf)
-    }
-
-    /// The reference crate on the CPU: the fallback, and the semantics the GPU
-    /// path reproduces (codes: signature first, then key, then pairing --
-    /// utils/verify-bls-signatures/src/lib.rs:243-247).
-    pub fn cpu_code(sig: &[u8], msg: &[u8], key: &[u8]) -> u8 {
-        use ic_verify_bls_signature::{InvalidPublicKey, InvalidSignature, PublicKey, Signature};
-        let s = match Signature::deserialize(sig) {
-            Ok(s) => s,
-            Err(InvalidSignature::WrongLength) => return 1,
-            Err(_) => return 2,
-        };
-        let k = match PublicKey::deserialize(key) {
-            Ok(k) => k,
-            Err(InvalidPublicKey::WrongLength) => return 3,
-            Err(_) => return 4,
-        };
-        if k.verify(msg, &s).is_ok() { 0 } else { 5 }
-    }
-
-    /// Codes for a batch: cache hits first, the rest in one GPU batch
-    /// (cess_bls_verify_batch_var), the CPU if the GPU is absent or fails.
-    pub fn batch_codes(st: &GpuState, sigs: &[Vec<u8>], msgs: &[Vec<u8>], keys: &[Vec<u8>]) -> Vec<u8> {
-        let n = sigs.len();
-        let mut codes = vec![u8::MAX; n];
-        let mut miss = Vec::new();
-        {
-            let cache = st.cache.lock();
-            for i in 0..n {
-                match cache.get(&record_key(&sigs[i], &msgs[i], &keys[i])) {
-                    Some(&c) => codes[i] = c,
-                    None => miss.push(i),
-                }
-            }
-        }
-        if miss.is_empty() {
-            return codes;
-        }
-        let recs: Vec<(&[u8], &[u8], &[u8])> =
-            miss.iter().map(|&i| (&sigs[i][..], &msgs[i][..], &keys[i][..])).collect();
-        let gpu = st.verifier.lock().as_mut().and_then(|v| v.verify_batch(&recs).ok());
-        let mut cache = st.cache.lock();
-        for (j, &i) in miss.iter().enumerate() {
-            let c = match &gpu {
-                Some(v) => v.codes[j],
-                None => cpu_code(&sigs[i], &msgs[i], &keys[i]),
-            };
-            codes[i] = c;
-            cache.insert(record_key(&sigs[i], &msgs[i], &keys[i]), c);
-        }
-        codes
-    }
 }
 
 /// Host functions: `gpu_verify::verify_bls(..)` etc. in the runtime.
 #[runtime_interface]
 pub trait GpuVerify {
     /// `cp_enclave_verify::verify_bls(key, msg, sig)` (primitives/enclave-verify/
-    /// src/lib.rs:230-235) without its panics: `None` where the reference
-    /// unwraps a key or signature that does not deserialize, else the verdict.
-    fn verify_bls(&mut self, key: &[u8], msg: &[u8], sig: &[u8]) -> Option<bool> {
+    /// src/lib.rs:230-235) on the GPU: HOOK_TRUE / HOOK_FALSE for a verdict,
+    /// HOOK_UNAVAILABLE otherwise -- including records the reference would
+    /// panic on (key, then signature, not deserializing), so the panic stays
+    /// the runtime's own.
+    fn verify_bls(&mut self, key: &[u8], msg: &[u8], sig: &[u8]) -> u8 {
         let code = self.verify_bls_batch(vec![sig.to_vec()], vec![msg.to_vec()], vec![key.to_vec()])[0];
         match code {
-            0 => Some(true),
-            5 => Some(false),
-            _ => None,
+            BLS_OK => HOOK_TRUE,
+            BLS_PAIRING_FAIL => HOOK_FALSE,
+            _ => HOOK_UNAVAILABLE,
         }
     }
 
-    /// Batch form for node-side callers: one verdict code per record
-    /// (sigs[i], msgs[i], keys[i]), codes as in include/cess_bls.h.
+    /// Batch form for node-side callers: one code per record (sigs[i],
+    /// msgs[i], keys[i]), codes as in include/cess_bls.h, BLS_UNAVAILABLE
+    /// without a GPU verdict.
     fn verify_bls_batch(&mut self, sigs: Vec<Vec<u8>>, msgs: Vec<Vec<u8>>, keys: Vec<Vec<u8>>) -> Vec<u8> {
-        assert!(sigs.len() == msgs.len() && msgs.len() == keys.len());
+        if sigs.len() != msgs.len() || msgs.len() != keys.len() {
+            return sp_std::vec![BLS_UNAVAILABLE; sigs.len().max(msgs.len()).max(keys.len())];
+        }
         match self.extension::<ext::GpuVerifierExt>() {
-            Some(e) => ext::batch_codes(&e.0, &sigs, &msgs, &keys),
-            None => (0..sigs.len()).map(|i| ext::cpu_code(&sigs[i], &msgs[i], &keys[i])).collect(),
+            Some(e) => {
+                let recs: Vec<(&[u8], &[u8], &[u8])> =
+                    (0..sigs.len()).map(|i| (&sigs[i][..], &msgs[i][..], &keys[i][..])).collect();
+                e.0.batch_codes(&recs)
+            }
+            None => sp_std::vec![BLS_UNAVAILABLE; sigs.len()],
         }
     }
 
     /// `cp_enclave_verify::verify_rsa(key, msg, sig)` (primitives/enclave-verify/
-    /// src/lib.rs:221-228) without its panic: `None` where the SPKI key does
-    /// not parse.  Podr2 checks are single calls; the GPU batch form is
-    /// `Verifier::verify_rsa_batch` for node-side batchers.
-    fn verify_rsa(&mut self, key: &[u8], msg: &[u8], sig: &[u8]) -> Option<bool> {
-        if let Some(e) = self.extension::<ext::GpuVerifierExt>() {
-            if let Some(v) = e.0.verifier.lock().as_mut() {
-                match v.verify_rsa(key, msg, sig) {
-                    Ok(ok) => return Some(ok),
-                    Err(verify_bls_signatures_gpu::Error::BadKey) => return None,
-                    Err(_) => {}   // infrastructure: fall through to the CPU
-                }
-            }
+    /// src/lib.rs:221-228) on the GPU: HOOK_TRUE / HOOK_FALSE, or
+    /// HOOK_UNAVAILABLE (no GPU, a key the GPU cannot verify or parse).
+    fn verify_rsa(&mut self, key: &[u8], msg: &[u8], sig: &[u8]) -> u8 {
+        match self.extension::<ext::GpuVerifierExt>().and_then(|e| e.0.rsa(key, msg, sig)) {
+            Some(true) => HOOK_TRUE,
+            Some(false) => HOOK_FALSE,
+            None => HOOK_UNAVAILABLE,
         }
-        use rsa::{pkcs8::DecodePublicKey, Pkcs1v15Sign, PublicKey, RsaPublicKey};
-        let pk = RsaPublicKey::from_public_key_der(key).ok()?;
-        Some(pk.verify(Pkcs1v15Sign::new_raw(), msg, sig).is_ok())
+    }
+}
+
+/// What the runtime calls (wasm and native alike): the GPU's verdict when the
+/// node has one, else the reference's own code path, unchanged.  The
+/// `cp-enclave-verify` dependency here is the runtime's existing wasm
+/// verifier, not part of the node-side hook.
+pub mod runtime {
+    use super::*;
+
+    /// Drop-in for `cp_enclave_verify::verify_bls(key, msg, sig)`.
+    pub fn verify_bls(key: &[u8], msg: &[u8], sig: &[u8]) -> bool {
+        match gpu_verify::verify_bls(key, msg, sig) {
+            HOOK_TRUE => true,
+            HOOK_FALSE => false,
+            _ => cp_enclave_verify::verify_bls(key, msg, sig),
+        }
+    }
+
+    /// Drop-in for `cp_enclave_verify::verify_rsa(key, msg, sig)`.
+    pub fn verify_rsa(key: &[u8], msg: &[u8], sig: &[u8]) -> bool {
+        match gpu_verify::verify_rsa(key, msg, sig) {
+            HOOK_TRUE => true,
+            HOOK_FALSE => false,
+            _ => cp_enclave_verify::verify_rsa(key, msg, sig),
+        }
+    }
+}
+
+sp_api::decl_runtime_apis! {
+    /// What the node-side batcher asks the runtime (patches/node_batcher.rs):
+    /// the (signature, message, key) records that the given pool transactions
+    /// will ask `gpu_verify::verify_bls` about -- the runtime has the storage
+    /// (TEE keys, challenge snapshot) to build them.  Implemented in the
+    /// runtime by `decode_verify_record` (patches/audit.rs).
+    pub trait GpuVerifyRecords {
+        fn verify_records(xts: Vec<Block::Extrinsic>) -> Vec<(Vec<u8>, Vec<u8>, Vec<u8>)>;
     }
 }

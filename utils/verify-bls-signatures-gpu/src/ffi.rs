@@ -15,6 +15,7 @@ pub const CESS_BLS_E_BUSY: c_int = -6;
 pub const CESS_BLS_E_BAD_KEY: c_int = -7;
 pub const CESS_BLS_E_BAD_SIG: c_int = -8;
 pub const CESS_BLS_E_NO_COMM: c_int = -9;
+pub const CESS_BLS_E_COMM: c_int = -11;
 
 pub const CODE_OK: u8 = 0;
 pub const CODE_SIG_LEN: u8 = 1;
@@ -22,6 +23,11 @@ pub const CODE_SIG_POINT: u8 = 2;
 pub const CODE_PK_LEN: u8 = 3;
 pub const CODE_PK_POINT: u8 = 4;
 pub const CODE_PAIRING_FAIL: u8 = 5;
+/// no verdict (cache path without a device / failed batch): the caller decides
+pub const CODE_UNAVAILABLE: u8 = 0xff;
+pub const CESS_BLS_KIND_SIG: c_int = 0;
+pub const CESS_BLS_KIND_PK: c_int = 1;
+pub const CESS_BLS_COMM_NAME_BYTES: usize = 64;
 
 pub const CESS_BLS_F_PROFILE: u32 = 1;
 pub const CESS_BLS_F_STRICT_IDENTITY: u32 = 2;
@@ -41,6 +47,14 @@ pub struct cess_bls_config {
 
 #[repr(C)]
 pub struct cess_bls_ctx {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct cess_bls_comm {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct cess_bls_cache {
     _private: [u8; 0],
 }
 
@@ -103,6 +117,32 @@ extern "C" {
                                              stats4: *mut u64, global_ok_out: *mut c_int) -> c_int;
     pub fn cess_bls_comm_barrier(ctx: *mut cess_bls_ctx) -> c_int;
     pub fn cess_bls_comm_max_f64(ctx: *mut cess_bls_ctx, value: *mut f64) -> c_int;
+    pub fn cess_bls_comm_kind(ctx: *mut cess_bls_ctx) -> *const c_char;
+    // host shared-memory transport of the sharded entry points (ranks on one host)
+    pub fn cess_bls_comm_shm_name(name_out: *mut c_char) -> c_int;
+    pub fn cess_bls_comm_init_shm(ctx: *mut cess_bls_ctx, nranks: c_int, rank: c_int, name: *const c_char) -> c_int;
+    pub fn cess_bls_comm_open_shm(name: *const c_char, nranks: c_int, rank: c_int,
+                                  out: *mut *mut cess_bls_comm) -> c_int;
+    pub fn cess_bls_comm_close(comm: *mut cess_bls_comm);
+    pub fn cess_bls_comm_agree(comm: *mut cess_bls_comm, status: c_int, agreed_out: *mut c_int) -> c_int;
+    pub fn cess_bls_comm_gather_verdicts(comm: *mut cess_bls_comm, n_total: u64, shard_codes: *const u8,
+                                         codes_out: *mut u8, bitmap_out: *mut u64) -> c_int;
+    // Signature::deserialize (:138-152) / PublicKey::deserialize (:68-82) alone
+    pub fn cess_bls_deserialize_batch(ctx: *mut cess_bls_ctx, kind: c_int, n: usize, data: *const u8,
+                                      offsets: *const u64, codes_out: *mut u8) -> c_int;
+    // bounded verdict cache (node host function + batcher)
+    pub fn cess_bls_cache_create(capacity: usize, out: *mut *mut cess_bls_cache) -> c_int;
+    pub fn cess_bls_cache_destroy(cache: *mut cess_bls_cache);
+    pub fn cess_bls_cache_clear(cache: *mut cess_bls_cache) -> c_int;
+    pub fn cess_bls_cache_size(cache: *mut cess_bls_cache) -> usize;
+    pub fn cess_bls_cache_verify_var(cache: *mut cess_bls_cache, ctx: *mut cess_bls_ctx, n: usize,
+                                     sig_data: *const u8, sig_offsets: *const u64, pk_data: *const u8,
+                                     pk_offsets: *const u64, msgs: *const u8, msg_offsets: *const u64,
+                                     codes_out: *mut u8, stats3: *mut u64) -> c_int;
+    pub fn cess_bls_cache_insert_var(cache: *mut cess_bls_cache, n: usize, sig_data: *const u8,
+                                     sig_offsets: *const u64, pk_data: *const u8, pk_offsets: *const u64,
+                                     msgs: *const u8, msg_offsets: *const u64, codes: *const u8) -> c_int;
+    pub fn cess_bls_sha256(data: *const u8, len: usize, out: *mut u8) -> c_int;
     // device memory on the context's GPU
     pub fn cess_bls_device_alloc(ctx: *mut cess_bls_ctx, bytes: usize, d_out: *mut *mut c_void) -> c_int;
     pub fn cess_bls_device_free(ctx: *mut cess_bls_ctx, d: *mut c_void) -> c_int;
@@ -130,6 +170,9 @@ extern "C" {
                                  codes_out: *mut u8, bitmap_out: *mut u64) -> c_int;
     pub fn cess_rsa_verify(ctx: *mut cess_bls_ctx, key_der: *const u8, key_len: usize, msg: *const u8,
                            msg_len: usize, sig: *const u8, sig_len: usize, ok_out: *mut c_int) -> c_int;
+    pub fn cess_rsa_verify_batch_device(ctx: *mut cess_bls_ctx, n: usize, d_key_idx: *const u32, d_sigs: *const u8,
+                                        d_sig_offsets: *const u64, d_msgs: *const u8, d_msg_offsets: *const u64,
+                                        d_codes: *mut u8, stream: *mut c_void) -> c_int;
 }
 
 pub const CESS_RSA_E_UNSUPPORTED: c_int = -10;

@@ -30,6 +30,12 @@ pub enum Error {
     BadKey,
     BadSig,
     NoComm,
+    /// shared-memory communicator: a peer timed out / the transport failed
+    Comm,
+    /// RSA: the key parses (the reference accepts it) but the GPU cannot
+    /// verify it (> 2048-bit, even modulus, non-NULL SPKI parameters); the
+    /// caller's own path decides (include/cess_rsa.h)
+    Unsupported,
     Other(i32),
 }
 
@@ -45,6 +51,8 @@ impl Error {
             ffi::CESS_BLS_E_BAD_KEY => Error::BadKey,
             ffi::CESS_BLS_E_BAD_SIG => Error::BadSig,
             ffi::CESS_BLS_E_NO_COMM => Error::NoComm,
+            ffi::CESS_BLS_E_COMM => Error::Comm,
+            ffi::CESS_RSA_E_UNSUPPORTED => Error::Unsupported,
             s => Error::Other(s),
         }
     }
@@ -59,6 +67,8 @@ impl Error {
             Error::BadKey => ffi::CESS_BLS_E_BAD_KEY,
             Error::BadSig => ffi::CESS_BLS_E_BAD_SIG,
             Error::NoComm => ffi::CESS_BLS_E_NO_COMM,
+            Error::Comm => ffi::CESS_BLS_E_COMM,
+            Error::Unsupported => ffi::CESS_RSA_E_UNSUPPORTED,
             Error::Other(s) => s,
         };
         unsafe { CStr::from_ptr(ffi::cess_bls_status_string(st)) }.to_string_lossy().into_owned()
@@ -246,11 +256,37 @@ impl Verifier {
         })?;
         Ok(v)
     }
+    /// Host shared-memory transport instead of RCCL (ranks on one host, which
+    /// may share a GPU); `name` from `Verifier::comm_shm_name` on one rank.
+    pub fn comm_init_shm(&mut self, nranks: i32, rank: i32, name: &CStr) -> Result<(), Error> {
+        check(unsafe { ffi::cess_bls_comm_init_shm(self.ctx, nranks, rank, name.as_ptr()) })
+    }
+    pub fn comm_shm_name() -> Result<std::ffi::CString, Error> {
+        let mut buf = [0 as core::ffi::c_char; ffi::CESS_BLS_COMM_NAME_BYTES];
+        check(unsafe { ffi::cess_bls_comm_shm_name(buf.as_mut_ptr()) })?;
+        Ok(unsafe { CStr::from_ptr(buf.as_ptr()) }.to_owned())
+    }
     /// Records [begin, end) of `rank`'s shard and the bitmap words per rank.
     pub fn shard_range(n: u64, nranks: i32, rank: i32) -> Result<(u64, u64, u64), Error> {
         let (mut b, mut e, mut w) = (0u64, 0u64, 0u64);
         check(unsafe { ffi::cess_bls_shard_range(n, nranks, rank, &mut b, &mut e, &mut w) })?;
         Ok((b, e, w))
+    }
+
+    /// Signature::deserialize / PublicKey::deserialize over a batch, decode
+    /// kernels only (no pairing): codes 0, SIG_LEN / SIG_POINT or PK_LEN / PK_POINT.
+    pub fn deserialize_codes(&mut self, kind: c_int, encodings: &[&[u8]]) -> Result<Vec<u8>, Error> {
+        let mut data = Vec::new();
+        let o = offsets(encodings.iter().copied(), &mut data);
+        let mut codes = vec![0u8; encodings.len()];
+        if encodings.is_empty() {
+            return Ok(codes);
+        }
+        check(unsafe {
+            ffi::cess_bls_deserialize_batch(self.ctx, kind, encodings.len(), data.as_ptr(), o.as_ptr(),
+                                            codes.as_mut_ptr())
+        })?;
+        Ok(codes)
     }
 
     /// `cp_enclave_verify::verify_bls(key, msg, sig)` without the panics.
@@ -352,17 +388,6 @@ fn with_default<R>(f: impl FnOnce(&mut Verifier) -> R) -> R {
     f(&mut v)
 }
 
-const ID_SIG: [u8; 48] = {
-    let mut b = [0u8; 48];
-    b[0] = 0xc0;
-    b
-};
-const ID_PK: [u8; 96] = {
-    let mut b = [0u8; 96];
-    b[0] = 0xc0;
-    b
-};
-
 #[derive(Copy, Clone, Debug, Eq, PartialEq)]
 pub enum InvalidPublicKey {
     WrongLength,
@@ -394,7 +419,9 @@ impl PublicKey {
         if bytes.len() != Self::BYTES {
             return Err(InvalidPublicKey::WrongLength);
         }
-        let code = with_default(|v| v.verify_code(&ID_SIG, b"", bytes)).expect("verifier");
+        // decode kernels only (cess_bls_deserialize_batch): a decode's latency,
+        // not a whole verification's
+        let code = with_default(|v| v.deserialize_codes(ffi::CESS_BLS_KIND_PK, &[bytes])).expect("verifier")[0];
         if code == ffi::CODE_PK_POINT {
             return Err(InvalidPublicKey::InvalidPoint);
         }
@@ -432,7 +459,7 @@ impl Signature {
         if bytes.len() != Self::BYTES {
             return Err(InvalidSignature::WrongLength);
         }
-        let code = with_default(|v| v.verify_code(bytes, b"", &ID_PK)).expect("verifier");
+        let code = with_default(|v| v.deserialize_codes(ffi::CESS_BLS_KIND_SIG, &[bytes])).expect("verifier")[0];
         if code == ffi::CODE_SIG_POINT {
             return Err(InvalidSignature::InvalidPoint);
         }
@@ -466,6 +493,19 @@ pub struct PrivateKey {
 
 impl PrivateKey {
     pub const BYTES: usize = 32;
+    /// PrivateKey::random (src/lib.rs:185-198): 32 bytes from the OS CSPRNG
+    /// (getrandom), redrawn until the big-endian value is below r -- the
+    /// reference's rejection sampling through `Scalar::from_bytes`.  Zero is
+    /// accepted, as there (it yields the identity key).
+    pub fn random() -> Self {
+        loop {
+            let mut sk = [0u8; 32];
+            getrandom::getrandom(&mut sk).expect("getrandom");
+            if let Ok(k) = Self::deserialize(&sk) {
+                return k;
+            }
+        }
+    }
     /// PrivateKey::deserialize (src/lib.rs:208-223)
     pub fn deserialize(bytes: &[u8]) -> Result<Self, InvalidPrivateKey> {
         if bytes.len() != Self::BYTES {
@@ -529,18 +569,104 @@ pub fn verify_bls(key: &[u8], msg: &[u8], sig: &[u8]) -> Result<(), ()> {
 /// `cp_enclave_verify::verify_rsa(key, msg, sig)` (primitives/enclave-verify/
 /// src/lib.rs:221-228) with the reference's semantics: panics if the key does
 /// not parse as SubjectPublicKeyInfo DER.
+///
+/// DIVERGENCE (documented): a key the reference parses but the GPU
+/// cannot verify (> 2048-bit modulus, even modulus, non-NULL SPKI parameters;
+/// `Error::Unsupported`) also panics here, where the reference returns a
+/// verdict.  Callers that must not panic on such keys use `try_verify_rsa` and
+/// route `Err(Error::Unsupported)` to their own path (the node hook answers
+/// "unavailable" and the runtime's unchanged verifier decides).  This crate
+/// links no CPU RSA implementation.
 pub fn verify_rsa(key: &[u8], msg: &[u8], sig: &[u8]) -> bool {
-    match with_default(|v| v.verify_rsa(key, msg, sig)) {
+    match try_verify_rsa(key, msg, sig) {
         Ok(ok) => ok,
         Err(e) => panic!("called `Result::unwrap()` on an `Err` value: {}", e.message()),
+    }
+}
+
+/// `verify_rsa` without panics: `Err(BadKey)` where the reference panics,
+/// `Err(Unsupported)` where only the GPU cannot decide.
+pub fn try_verify_rsa(key: &[u8], msg: &[u8], sig: &[u8]) -> Result<bool, Error> {
+    with_default(|v| v.verify_rsa(key, msg, sig))
+}
+
+/// Bounded verdict cache of the C library (cess_bls_cache_*): SHA-256 of the
+/// length-prefixed (sig, msg, key) -> verdict code; oldest entries evicted
+/// first at capacity.  Thread-safe (the library locks it).
+pub struct VerdictCache {
+    cache: *mut ffi::cess_bls_cache,
+}
+
+unsafe impl Send for VerdictCache {}
+unsafe impl Sync for VerdictCache {}
+
+/// What `VerdictCache::verify` reports next to the codes.
+#[derive(Clone, Copy, Debug, Default, Eq, PartialEq)]
+pub struct CacheStats {
+    pub hits: u64,
+    pub verified: u64,
+    pub evicted: u64,
+}
+
+impl VerdictCache {
+    pub fn new(capacity: usize) -> Result<Self, Error> {
+        let mut p = core::ptr::null_mut();
+        check(unsafe { ffi::cess_bls_cache_create(capacity, &mut p) })?;
+        Ok(VerdictCache { cache: p })
+    }
+    pub fn len(&self) -> usize {
+        unsafe { ffi::cess_bls_cache_size(self.cache) }
+    }
+    pub fn clear(&self) {
+        unsafe { ffi::cess_bls_cache_clear(self.cache) };
+    }
+    /// Codes for records of any lengths: cached verdicts, the misses verified
+    /// in one batch on `verifier` and cached.  With no verifier, or when that
+    /// batch fails, the misses are `ffi::CODE_UNAVAILABLE` (never cached) and
+    /// the batch's error is returned beside the codes.
+    pub fn verify(&self, verifier: Option<&mut Verifier>, records: &[(&[u8], &[u8], &[u8])])
+                  -> (Vec<u8>, CacheStats, Result<(), Error>) {
+        let n = records.len();
+        let mut codes = vec![ffi::CODE_UNAVAILABLE; n];
+        if n == 0 {
+            return (codes, CacheStats::default(), Ok(()));
+        }
+        let (mut sd, mut pd, mut md) = (Vec::new(), Vec::new(), Vec::new());
+        let so = offsets(records.iter().map(|r| r.0), &mut sd);
+        let mo = offsets(records.iter().map(|r| r.1), &mut md);
+        let po = offsets(records.iter().map(|r| r.2), &mut pd);
+        let ctx = verifier.map(|v| v.ctx).unwrap_or(core::ptr::null_mut());
+        let mut st3 = [0u64; 3];
+        let st = unsafe {
+            ffi::cess_bls_cache_verify_var(self.cache, ctx, n, sd.as_ptr(), so.as_ptr(), pd.as_ptr(), po.as_ptr(),
+                                           md.as_ptr(), mo.as_ptr(), codes.as_mut_ptr(), st3.as_mut_ptr())
+        };
+        (codes, CacheStats { hits: st3[0], verified: st3[1], evicted: st3[2] }, check(st))
+    }
+    /// Insert verdicts obtained elsewhere (e.g. gathered codes of a sharded batch).
+    pub fn insert(&self, records: &[(&[u8], &[u8], &[u8])], codes: &[u8]) -> Result<(), Error> {
+        assert_eq!(records.len(), codes.len());
+        let (mut sd, mut pd, mut md) = (Vec::new(), Vec::new(), Vec::new());
+        let so = offsets(records.iter().map(|r| r.0), &mut sd);
+        let mo = offsets(records.iter().map(|r| r.1), &mut md);
+        let po = offsets(records.iter().map(|r| r.2), &mut pd);
+        check(unsafe {
+            ffi::cess_bls_cache_insert_var(self.cache, records.len(), sd.as_ptr(), so.as_ptr(), pd.as_ptr(),
+                                           po.as_ptr(), md.as_ptr(), mo.as_ptr(), codes.as_ptr())
+        })
+    }
+}
+
+impl Drop for VerdictCache {
+    fn drop(&mut self) {
+        unsafe { ffi::cess_bls_cache_destroy(self.cache) }
     }
 }
 
 #[cfg(test)]
 mod tests {
     // The reference's KATs (utils/verify-bls-signatures/tests/tests.rs) run
-    // unchanged against this crate on a box with an MI355X: add
-    // `use ic_verify_bls_signature_gpu::*;` to a copy of tests.rs.
+    // against this crate in tests/kat.rs on a box with cargo and an MI355X.
     use super::*;
 
     #[test]

@@ -183,17 +183,23 @@ def load_opcount():
         return json.load(f)
 
 
-def load_pmc_traffic(sha: str):
+def load_pmc_traffic(sha: str, kernel=None, n=None):
     """HBM bytes per launch from a committed rocprofv3 PMC summary
     (profiles/*_pmc_traffic.json) measured on THIS library build (same
-    SHA-256); None when no profile of this build exists."""
+    SHA-256), for `kernel` at launch size `n` when given; None when no profile
+    of this build exists."""
     import glob
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
         with open(p) as f:
             d = json.load(f)
-        if d.get("lib_sha256") == sha:
-            d["_file"] = os.path.relpath(p, ROOT)
-            return d
+        if d.get("lib_sha256") != sha:
+            continue
+        if kernel is not None and kernel not in d.get("all", {}):
+            continue
+        if n is not None and d.get("n") != n:
+            continue
+        d["_file"] = os.path.relpath(p, ROOT)
+        return d
     return None
 
 
@@ -353,11 +359,14 @@ def run_rsa(args, ctx, rank, world):
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
+    ctx.stage_stats(reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     ctx.synchronize()
     elapsed = time.perf_counter() - t0
+    # HIP events around each launch on its stream (CESS_BLS_F_PROFILE)
+    st = {k: v for k, v in ctx.stage_stats(reset=True).items() if v[1] > 0}
     codes = np.frombuffer(ctx.from_device(d_codes, n), dtype=np.uint8)
     ok = bool((codes == expect).all())
     if world > 1:
@@ -365,8 +374,13 @@ def run_rsa(args, ctx, rank, world):
         ok = ctx.comm_max(0.0 if ok else 1.0) == 0.0
     if rank == 0:
         value = n * world * args.steps / elapsed
-        per_gpu = value / world
-        achieved = per_gpu * RSA2048_ALG_MADS
+        ver_ms, ver_launches = st["k_rsa_verify"]
+        assert ver_launches == args.steps, st
+        verify_ms = ver_ms / ver_launches                  # average launch duration, HIP events
+        achieved = n * RSA2048_ALG_MADS / (verify_ms * 1e-3)
+        sha = lib_sha256()
+        pmc = load_pmc_traffic(sha, "k_rsa_verify_2048", n)
+        kd = (pmc or {}).get("all", {}).get("k_rsa_verify_2048", {})
         cpu = None
         if world == 1 and args.cpu_sample > 0:
             kn, ke = bls_rsa_key(key)
@@ -381,14 +395,19 @@ def run_rsa(args, ctx, rank, world):
             "config": {"workload": f"SURVEY §8(f) rank 4, cp_enclave_verify::verify_rsa: {n} sigs per GPU, inputs in HBM",
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
-            "roofline": {"bound": "valu-int", "kernel": "k_rsa_verify_2048 (+k_rsa_classify)",
+            "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
+            "roofline": {"bound": "valu-int", "kernel": "k_rsa_verify_2048",
                          "achieved": achieved / 1e12, "peak": PEAK_MADS / 1e12,
                          "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)", "frac": achieved / PEAK_MADS,
-                         "traffic": None, "alg_mads_per_sig": RSA2048_ALG_MADS,
-                         "note": "timed over whole launches (classify + verify); 28-bit limbs issue 74^2-based "
-                                 "products (1.34x the 32-bit count)"},
+                         "traffic": kd.get("hbm_bytes_per_launch"), "traffic_source": pmc["_file"] if pmc else None,
+                         "pmc_valu_active_per_wave": (kd["SQ_ACTIVE_INST_VALU"] / kd["SQ_WAVE_CYCLES"]
+                                                      if kd.get("SQ_WAVE_CYCLES") else None),
+                         "alg_mads_per_sig": RSA2048_ALG_MADS,
+                         "whole_step_frac": value / world * RSA2048_ALG_MADS / PEAK_MADS,
+                         "note": "achieved = algorithmic mads of one launch / its HIP-event duration; 28-bit limbs "
+                                 "issue 74^2-based products (1.34x the 32-bit count)"},
             "cpu_baseline": cpu,
-            "runtime": runtime_provenance(),
+            "runtime": dict(runtime_provenance(), lib_sha256=sha),
         }), flush=True)
     for p in (d_idx, d_sig, d_soff, d_msg, d_moff, d_codes):
         ctx.device_free(p)
@@ -512,7 +531,7 @@ def main():
 
     n = args.n or (N1_DEFAULT if world == 1 else NPER_MULTI)
     if args.mode == "rsa":
-        ctx = bls.Context(device=local, max_batch=1 << 16)
+        ctx = bls.Context(device=local, max_batch=1 << 16, profile=True)
         if world > 1:
             comm_setup(ctx, rank, world, args.transport)
         run_rsa(args, ctx, rank, world)
@@ -578,7 +597,7 @@ def main():
         ctx.comm_barrier()
     elapsed = time.perf_counter() - t0
     # per-launch HIP events on each kernel's own stream, timed region only
-    stats = ctx.stage_stats(reset=True)
+    stats = {k: v for k, v in ctx.stage_stats(reset=True).items() if v[1] > 0}
     if keyed:   # the keyed pipeline runs k_merge_pk in k_decode_pk's slot and has no per-signature prepare
         stats["k_merge_pk"] = stats.pop("k_decode_pk")
         stats.pop("k_prepare", None)
@@ -611,7 +630,7 @@ def main():
         alg = (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL * chunk
         achieved = alg / (dom_ms * 1e-3)
         sha = lib_sha256()
-        pmc = load_pmc_traffic(sha)
+        pmc = load_pmc_traffic(sha, dom, chunk)
         traffic = valu_active = None
         if pmc and pmc.get("n") == chunk:
             kd = pmc.get("all", {}).get(dom) or {}

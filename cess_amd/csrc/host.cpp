@@ -15,7 +15,8 @@
 using namespace cess_host;
 
 namespace {
-const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk", "k_hash", "k_prepare", "k_miller", "k_final"};
+const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk", "k_hash",          "k_prepare",
+                                 "k_miller",     "k_final",     "k_rsa_classify", "k_rsa_verify"};
 }
 
 extern "C" const char* cess_bls_version(void) { return "cess_amd-bls 0.2 (gfx950)"; }

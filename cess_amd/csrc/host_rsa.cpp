@@ -235,18 +235,29 @@ static int rsa_run(cess_bls_ctx* c, RsaTable& T, hipStream_t s, uint64_t n, cons
   if (S.lists.ensure(2 * n * 4) | S.counts.ensure(16) | S.base.ensure(n * RSA_LMAX * 4)) return CESS_BLS_E_OOM;
   if (T.keys.ensure(sizeof(RsaKeyDev)) | T.ok.ensure(1)) return CESS_BLS_E_OOM;
   HIPCHK(hipMemsetAsync(S.counts.p, 0, 16, s));
+  // per-launch HIP events on s (CESS_BLS_F_PROFILE): bench.py's roofline
+  // takes the verification kernel's duration from them
+  hipEvent_t a;
+  int r = prof_begin(c, s, ST_RSA_CLASSIFY, &a);
+  if (r) return r;
   hipLaunchKernelGGL(k_rsa_classify, dim3(grid_for(n)), dim3(kBlock), 0, s, n, d_idx, T.n,
                      (const RsaKeyDev*)T.keys.as<RsaKeyDev>(), (const uint8_t*)T.ok.as<uint8_t>(), d_soffs, d_moffs,
                      d_codes, S.lists.as<uint32_t>(), S.counts.as<uint32_t>());
+  r = prof_end(c, s, ST_RSA_CLASSIFY, a);
+  if (r) return r;
   const uint32_t* cnt = S.counts.as<uint32_t>();
   const uint32_t* L = S.lists.as<uint32_t>();
   const RsaKeyDev* K = T.keys.as<RsaKeyDev>();
   uint32_t* B = S.base.as<uint32_t>();
   // every class kernel covers n lanes; lanes past the class's count exit
+  r = prof_begin(c, s, ST_RSA_VERIFY, &a);
+  if (r) return r;
   hipLaunchKernelGGL(k_rsa_verify_2048, dim3(grid_for(n)), dim3(kBlock), 0, s, (uint32_t)n, cnt + 1, L + n, d_idx, K,
                      d_sigs, d_soffs, d_msgs, d_moffs, B, d_codes);
   hipLaunchKernelGGL(k_rsa_verify_1024, dim3(grid_for(n)), dim3(kBlock), 0, s, (uint32_t)n, cnt, L, d_idx, K, d_sigs,
                      d_soffs, d_msgs, d_moffs, B, d_codes);
+  r = prof_end(c, s, ST_RSA_VERIFY, a);
+  if (r) return r;
   HIPCHK(hipGetLastError());
   return CESS_BLS_OK;
 }
@@ -278,6 +289,8 @@ static int rsa_host(cess_bls_ctx* c, RsaTable& T, size_t n, const uint32_t* key_
   HIPCHK(hipMemcpyAsync(S.in_moffs.p, mo.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
   r = rsa_run(c, T, s, n, S.in_idx.as<uint32_t>(), S.in_sigs.as<uint8_t>(), S.in_soffs.as<uint64_t>(),
               S.in_msgs.as<uint8_t>(), S.in_moffs.as<uint64_t>(), S.out_codes.as<uint8_t>());
+  if (r) return r;
+  r = collect_profile(c, s);
   if (r) return r;
   std::vector<uint8_t> codes(n);
   HIPCHK(hipMemcpyAsync(codes.data(), S.out_codes.p, n, hipMemcpyDeviceToHost, s));
@@ -351,6 +364,8 @@ extern "C" int cess_rsa_verify_batch_device(cess_bls_ctx* c, size_t n, const uin
   int r = order_begin(c, s);
   if (r) return r;
   r = rsa_run(c, rsa_state(c).user, s, n, d_key_idx, d_sigs, d_sig_offsets, d_msgs, d_msg_offsets, d_codes);
+  if (r) return r;
+  r = collect_profile(c, s);   // no-op without CESS_BLS_F_PROFILE
   if (r) return r;
   return order_end(c, s);
 }

@@ -15,8 +15,8 @@
 using namespace cess_host;
 
 namespace {
-const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk", "k_hash",          "k_prepare",
-                                 "k_miller",     "k_final",     "k_rsa_classify", "k_rsa_verify"};
+const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk",    "k_hash",       "k_prepare", "k_miller",
+                                 "k_final",      "k_rsa_classify", "k_rsa_verify", "k_group"};
 }
 
 extern "C" const char* cess_bls_version(void) { return "cess_amd-bls 0.2 (gfx950)"; }
@@ -100,6 +100,16 @@ static uint64_t launch_records(uint64_t cap) {
   return std::min(cap, q);
 }
 
+// Batches of at most this many records run the lane-group path (k_group: one
+// signature per wave): below it the one-lane-per-signature
+// pipeline costs one lane's latency through six kernels whatever the batch
+// size.  Env CESS_BLS_SMALL_BATCH (0 disables).
+static uint64_t small_records() {
+  uint64_t v = 2048;
+  if (const char* e = getenv("CESS_BLS_SMALL_BATCH")) v = strtoull(e, nullptr, 10);
+  return v;
+}
+
 int cess_multi_create(const cess_bls_config* cfg, int ndev, cess_bls_ctx* c);   // host_multi.cpp
 
 extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** out) {
@@ -127,6 +137,7 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
   uint64_t cap = (cfg && cfg->max_batch) ? cfg->max_batch : (1ull << 20);
   c->cap = (cap + 63) & ~63ull;
   c->qcap = launch_records(c->cap);
+  c->small = std::min(small_records(), c->qcap);
   c->flags = cfg ? cfg->flags : 0;
   c->mode = cfg ? cfg->mode : CESS_BLS_MODE_PER_SIG;
   bool ok = hipSetDevice(c->device) == hipSuccess &&
@@ -277,6 +288,27 @@ int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8
         c->slot[k].coeffs.ensure(c->qcap * (uint64_t)CESS_W_COEFFS * 4))
       return CESS_BLS_E_OOM;
   const uint32_t strict = (c->flags & CESS_BLS_F_STRICT_IDENTITY) ? 1u : 0u;
+  if (n <= c->small) {
+    // small batch: decode + hash one lane per record, then one wave per record
+    // runs the Miller loop with the key's lines, the key's subgroup check and
+    // the final exponentiation (k_group)
+    StageSlot& S = c->slot[0];
+    const uint64_t q = c->qcap;
+    const unsigned g = grid_for(n);
+    uint8_t* inf = S.inf.as<uint8_t>();
+    LAUNCH(ST_DECODE_SIG, s, k_decode_sig, dim3(g), dim3(kBlock), 0, s, n, sigs, pre, codes, inf,
+           S.sig_aff.as<uint32_t>(), q);
+    LAUNCH(ST_DECODE_PK, s, k_decode_pk, dim3(g), dim3(kBlock), 0, s, n, pks, pre, codes, inf,
+           S.pk_aff.as<uint32_t>(), q, strict);
+    LAUNCH(ST_HASH, s, k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes,
+           S.h_aff.as<uint32_t>(), q);
+    LAUNCH(ST_GROUP, s, k_group, dim3((unsigned)n), dim3(64), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
+           (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
+           (const uint32_t*)S.pk_aff.as<uint32_t>(), q, codes, gt);
+    hipLaunchKernelGGL(k_codes_bitmap, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, bitmap);
+    HIPCHK(hipGetLastError());
+    return CESS_BLS_OK;
+  }
   auto light = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m, hipStream_t t) -> int {
     const unsigned g = grid_for(m);
     uint8_t* inf = S.inf.as<uint8_t>();

@@ -29,6 +29,10 @@ __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*,
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
 __global__ void k_hash_out(uint64_t, const uint8_t*, const uint64_t*, uint8_t*);
+// small-batch (latency) path (k_group.hip): one signature per wave
+__global__ void k_group(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                        uint64_t, uint8_t*, uint8_t*);
+__global__ void k_codes_bitmap(uint64_t, const uint8_t*, uint64_t*);
 // RLC batch mode (k_rlc.hip)
 __global__ void k_rlc_scale(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                             uint64_t, uint32_t*, uint32_t*, uint64_t, uint64_t);
@@ -41,7 +45,8 @@ __global__ void k_fp12_prod_segs(uint32_t, const uint32_t*, const uint4*, uint64
 
 namespace cess_host {
 
-enum Stage { ST_DECODE_SIG, ST_DECODE_PK, ST_HASH, ST_PREPARE, ST_MILLER, ST_FINAL, ST_RSA_CLASSIFY, ST_RSA_VERIFY, ST_N };
+enum Stage { ST_DECODE_SIG, ST_DECODE_PK, ST_HASH, ST_PREPARE, ST_MILLER, ST_FINAL, ST_RSA_CLASSIFY, ST_RSA_VERIFY,
+             ST_GROUP, ST_N };
 constexpr int kBlock = 256;
 
 inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -111,6 +116,7 @@ struct cess_bls_ctx {
   int device = 0;
   uint64_t cap = 0;    // records per host-API chunk (staging buffers)
   uint64_t qcap = 0;   // records per kernel launch (pipeline part; stage-buffer stride)
+  uint64_t small = 0;  // batches of at most this many records take the lane-group path (k_group)
   uint32_t flags = 0;
   uint32_t mode = CESS_BLS_MODE_PER_SIG;
   hipStream_t stream = nullptr;

@@ -105,7 +105,7 @@ static uint64_t launch_records(uint64_t cap) {
 // pipeline costs one lane's latency through six kernels whatever the batch
 // size.  Env CESS_BLS_SMALL_BATCH (0 disables).
 static uint64_t small_records() {
-  uint64_t v = 2048;
+  uint64_t v = 8192;   // measured crossover ~10 K (profiles/round3_c_latency.txt)
   if (const char* e = getenv("CESS_BLS_SMALL_BATCH")) v = strtoull(e, nullptr, 10);
   return v;
 }
@@ -143,6 +143,7 @@ extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** ou
   bool ok = hipSetDevice(c->device) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) == hipSuccess;
   for (int k = 0; k < 2 && ok; k++)
@@ -199,12 +200,14 @@ extern "C" void cess_bls_ctx_destroy(cess_bls_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
   }
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   delete c->xport;
   for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->done_ev, c->ev_start, c->ev_light[0], c->ev_light[1], c->ev_mill[0], c->ev_mill[1]})
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   delete c->rlc;
   cess_rsa_state_free(c);
   delete c;
@@ -292,19 +295,34 @@ int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8
     // small batch: decode + hash one lane per record, then one wave per record
     // runs the Miller loop with the key's lines, the key's subgroup check and
     // the final exponentiation (k_group)
+    // (the three light kernels are independent here: the key's code goes to
+    // code2 and k_group applies the reference precedence; they run on three
+    // streams, so a small batch costs the slowest of them, not their sum)
     StageSlot& S = c->slot[0];
     const uint64_t q = c->qcap;
     const unsigned g = grid_for(n);
     uint8_t* inf = S.inf.as<uint8_t>();
+    if (c->code2.ensure(q) | c->inf2.ensure(q)) return CESS_BLS_E_OOM;
+    uint8_t *code2 = c->code2.as<uint8_t>(), *inf2 = c->inf2.as<uint8_t>();
+    hipStream_t s2 = c->stream2, s3 = c->stream3;
+    HIPCHK(hipEventRecord(c->ev_start, s));
+    HIPCHK(hipStreamWaitEvent(s2, c->ev_start, 0));
+    HIPCHK(hipStreamWaitEvent(s3, c->ev_start, 0));
     LAUNCH(ST_DECODE_SIG, s, k_decode_sig, dim3(g), dim3(kBlock), 0, s, n, sigs, pre, codes, inf,
            S.sig_aff.as<uint32_t>(), q);
-    LAUNCH(ST_DECODE_PK, s, k_decode_pk, dim3(g), dim3(kBlock), 0, s, n, pks, pre, codes, inf,
+    HIPCHK(hipMemsetAsync(code2, 0, n, s2));
+    HIPCHK(hipMemsetAsync(inf2, 0, n, s2));
+    LAUNCH(ST_DECODE_PK, s2, k_decode_pk, dim3(g), dim3(kBlock), 0, s2, n, pks, pre, code2, inf2,
            S.pk_aff.as<uint32_t>(), q, strict);
-    LAUNCH(ST_HASH, s, k_hash, dim3(g), dim3(kBlock), 0, s, n, msgs, offs, (const uint8_t*)codes,
+    LAUNCH(ST_HASH, s3, k_hash, dim3(g), dim3(kBlock), 0, s3, n, msgs, offs, (const uint8_t*)nullptr,
            S.h_aff.as<uint32_t>(), q);
+    HIPCHK(hipEventRecord(c->ev_light[0], s2));
+    HIPCHK(hipEventRecord(c->ev_light[1], s3));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_light[0], 0));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_light[1], 0));
     LAUNCH(ST_GROUP, s, k_group, dim3((unsigned)n), dim3(64), 0, s, n, (const uint8_t*)codes, (const uint8_t*)inf,
-           (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
-           (const uint32_t*)S.pk_aff.as<uint32_t>(), q, codes, gt);
+           (const uint8_t*)code2, (const uint8_t*)inf2, (const uint32_t*)S.sig_aff.as<uint32_t>(),
+           (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)S.pk_aff.as<uint32_t>(), q, codes, gt);
     hipLaunchKernelGGL(k_codes_bitmap, dim3(g), dim3(kBlock), 0, s, n, (const uint8_t*)codes, bitmap);
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;
@@ -344,6 +362,7 @@ int cess_host::collect_profile(cess_bls_ctx* c, hipStream_t s) {
   if (!(c->flags & CESS_BLS_F_PROFILE)) return CESS_BLS_OK;
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipStreamSynchronize(c->stream2));
+  HIPCHK(hipStreamSynchronize(c->stream3));
   for (const ProfRec& p : c->prof) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));

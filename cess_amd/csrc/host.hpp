@@ -30,8 +30,8 @@ __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
 __global__ void k_sign(uint64_t, const uint8_t*, const uint8_t*, const uint64_t*, uint8_t*);
 __global__ void k_hash_out(uint64_t, const uint8_t*, const uint64_t*, uint8_t*);
 // small-batch (latency) path (k_group.hip): one signature per wave
-__global__ void k_group(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                        uint64_t, uint8_t*, uint8_t*);
+__global__ void k_group(uint64_t, const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*, const uint32_t*,
+                        const uint32_t*, const uint32_t*, uint64_t, uint8_t*, uint8_t*);
 __global__ void k_codes_bitmap(uint64_t, const uint8_t*, uint64_t*);
 // RLC batch mode (k_rlc.hip)
 __global__ void k_rlc_scale(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
@@ -126,6 +126,10 @@ struct cess_bls_ctx {
   // VGPRs) runs on the launch stream, so they share the CUs' issue slots.
   // Two stage slots alternate between parts.
   hipStream_t stream2 = nullptr;
+  // small-batch path: the key decode (stream2) and hashing (stream3) run
+  // beside the signature decode; the key decode's codes go to code2/inf2
+  hipStream_t stream3 = nullptr;
+  cess_host::DevBuf code2, inf2;
   hipEvent_t ev_start = nullptr, ev_light[2] = {}, ev_mill[2] = {};
   cess_host::StageSlot slot[2];
   cess_host::DevBuf pre, code, fval, fe_slots, bitmap, neg_g2;

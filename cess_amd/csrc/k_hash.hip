@@ -15,7 +15,7 @@ __global__ CESS_LB void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,
   g1a h;
   h.x = fp_zero();
   h.y = fp_one();
-  if (code[i] == 0) {
+  if (!code || code[i] == 0) {   // (no code array: the small-batch path hashes beside the decodes)
     uint64_t o = offs[i];
     uint32_t len = (uint32_t)(offs[i + 1] - o);
     h = hash_to_g1(msgs + o, len);

@@ -54,7 +54,7 @@ G2_GEN = (
      0x0606C4A02EA734CC32ACD2B02BC28B99CB3E287E85A763AF267492AB572E99AB3F370D275CEC1DA1AAA9075FF05F79BE),
 )
 
-LANES = 64
+LANES = 32   # operations per round: two lanes per operation (one per Fp2 component)
 MAX_LIN_TERMS = 12
 OP_MUL, OP_SQR, OP_LIN, OP_INV = 0, 1, 2, 3
 OP_NAMES = {OP_MUL: "MUL", OP_SQR: "SQR", OP_LIN: "LIN", OP_INV: "INV"}

@@ -17,6 +17,7 @@ namespace {
 struct HostRegs {
   std::vector<fp2>* S;
   fp2 ld(uint32_t s) const { return (*S)[s]; }
+  fp ld_comp(uint32_t s, uint32_t comp) const { return comp ? (*S)[s].c1 : (*S)[s].c0; }
 };
 fp load_raw(const uint32_t* x) {
   fp r;
@@ -33,18 +34,19 @@ int group_emu_run(const uint32_t* in, uint32_t* out) {
   const int ins[7] = {grp::IN_P0X, grp::IN_P0Y, grp::IN_P1X, grp::IN_P1Y, grp::IN_QX, grp::IN_QY, grp::IN_ONE};
   for (int k = 0; k < 7; k++) S[ins[k]] = {to_mont(load_raw(in + 24 * k)), to_mont(load_raw(in + 24 * k + 12))};
   HostRegs R{&S};
-  std::vector<std::pair<uint32_t, fp2>> wr;
+  // the kernel's lanes: lane 2 op + comp computes component comp of op
+  std::vector<std::pair<uint32_t, std::pair<uint32_t, fp>>> wr;
   for (int r = 0; r < grp::N_ROUNDS; r++) {
     const uint32_t h = grp::kRounds[r];
     const uint32_t kind = h & 0xffu, cnt = (h >> 8) & 0xffu, off = h >> 16;
     wr.clear();
-    for (uint32_t lane = 0; lane < cnt; lane++) {
-      const uint32_t* e = grp::kEnts[off + lane];
+    for (uint32_t lane = 0; lane < 2 * cnt; lane++) {
+      const uint32_t* e = grp::kEnts[off + (lane >> 1)];
       uint32_t d;
-      const fp2 v = group_eval(R, kind, e[0], e[1], e[2], e[3], &d);
-      wr.push_back({d, v});
+      const fp v = group_eval_comp(R, kind, e[0], e[1], e[2], e[3], lane & 1, &d);
+      wr.push_back({d, {lane & 1, v}});
     }
-    for (auto& w : wr) S[w.first] = w.second;
+    for (auto& w : wr) (w.second.first ? S[w.first].c1 : S[w.first].c0) = w.second.second;
   }
   const int outs[11] = {grp::OUT_TX,  grp::OUT_TY,  grp::OUT_TZ,  grp::OUT_PZX, grp::OUT_PZY, grp::OUT_GT0,
                         grp::OUT_GT1, grp::OUT_GT2, grp::OUT_GT3, grp::OUT_GT4, grp::OUT_GT5};

@@ -105,7 +105,7 @@ static uint64_t launch_records(uint64_t cap) {
 // pipeline costs one lane's latency through six kernels whatever the batch
 // size.  Env CESS_BLS_SMALL_BATCH (0 disables).
 static uint64_t small_records() {
-  uint64_t v = 4096;   // measured (profiles/round3_*_latency.txt)
+  uint64_t v = 8192;   // measured (profiles/round3_*_latency.txt)
   if (const char* e = getenv("CESS_BLS_SMALL_BATCH")) v = strtoull(e, nullptr, 10);
   return v;
 }

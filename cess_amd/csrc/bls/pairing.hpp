@@ -95,6 +95,36 @@ CESS_HD void normalize_line(coeff3& k) {
   k.c2 = fp2_one();
 }
 
+// normalize_line for a whole G2Prepared table (the keys of a distinct-key
+// table, built once and used by many signatures) with ONE Fp2 inversion:
+// Montgomery's simultaneous inversion, prefix products of the c2 kept in a
+// scratch Fp2 per line.  ld(k) / st(k, c) access line k, pre(k) / set_pre(k, v)
+// its scratch.  A table with a zero c2 (never for a key of G2 in practice, but
+// a crafted key could force one) is left unchanged and false returned; the
+// Miller loop then uses the general sparse product for it.
+template <class Ld, class St, class PreLd, class PreSt>
+CESS_HD bool normalize_lines(Ld&& ld, St&& st, PreLd&& pre, PreSt&& set_pre) {
+  fp2 prod = fp2_one();
+#pragma unroll 1
+  for (int k = 0; k < N_COEFFS; k++) {
+    set_pre(k, prod);
+    prod = mul(prod, ld(k).c2);
+  }
+  if (is_zero(prod)) return false;
+  fp2 iv = inv(prod);
+#pragma unroll 1
+  for (int k = N_COEFFS - 1; k >= 0; k--) {
+    coeff3 c = ld(k);
+    const fp2 ic2 = mul(iv, pre(k));   // 1 / c2_k
+    iv = mul(iv, c.c2);
+    c.c0 = mul(c.c0, ic2);
+    c.c1 = mul(c.c1, ic2);
+    c.c2 = fp2_one();
+    st(k, c);
+  }
+  return true;
+}
+
 CESS_HD fp12 ell(const fp12& f, const coeff3& k, const fp& px, const fp& py) {
   return mul_by_014(f, k.c2, mul_fp(k.c1, px), mul_fp(k.c0, py));
 }

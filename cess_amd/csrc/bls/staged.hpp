@@ -569,8 +569,10 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
 // normalize_line), pair 1 = (H(m), pk).  use0/use1:
 // the pair's points are both non-identity (identity terms contribute 1).
 // pt(pair) yields the pair's affine G1 point; src(pair, step) its coefficients.
+// norm1: pair 1's lines are normalised to c2 = 1 as well (a distinct-key table
+// after normalize_lines); otherwise they take the general sparse product.
 template <class S, class Pt, class Src>
-CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src) {
+CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1 = false) {
   set_one12(f);
 #pragma unroll 1
   for (int s = 0; s < N_COEFFS; s++) {
@@ -580,10 +582,10 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
       coeff3 k = src(pair, s);
       g1a p = pt(pair);
       fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
-      if (pair)
+      if (pair && !norm1)
         mul014(f, k.c2, c1, c4);
       else
-        mul014_one(f, c1, c4);   // -G2 table: lines normalised to c2 = 1
+        mul014_one(f, c1, c4);   // -G2 table (and normalised key tables): c2 = 1
       CESS_MEMBAR();
     }
     if (square_after_step(s)) sqr12(f);

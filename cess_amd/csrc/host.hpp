@@ -23,7 +23,8 @@ __global__ void k_hash(uint64_t, const uint8_t*, const uint64_t*, const uint8_t*
 __global__ void k_prepare(uint64_t, const uint32_t*, uint4*, uint64_t, uint8_t*, const uint8_t*);
 __global__ void k_norm_lines(uint4*);
 __global__ void k_miller(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                         const uint4*, uint4*, uint4*, uint64_t, const uint32_t*, uint64_t);
+                         const uint4*, uint4*, uint4*, uint64_t, const uint32_t*, uint64_t, const uint8_t*);
+__global__ void k_norm_keys(uint64_t, uint4*, uint32_t*, uint8_t*);
 __global__ void k_merge_pk(uint64_t, const uint32_t*, uint32_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*);
 __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
 __global__ void k_keygen(uint64_t, const uint8_t*, uint8_t*);
@@ -145,6 +146,8 @@ struct cess_bls_ctx {
   // distinct-key table (cess_bls_keys_load): decoded keys + G2Prepared rows, stride = nkeys
   uint32_t nkeys = 0;
   cess_host::DevBuf key_in, key_code, key_inf, key_aff, key_coeffs, in_idx;
+  // per key: 1 if its lines were normalised to c2 = 1 (k_norm_keys)
+  cess_host::DevBuf key_norm;
   // ordering of successive calls on possibly different streams: every entry
   // point waits for the previous call's work (done_ev on last_stream)
   hipEvent_t done_ev = nullptr;

@@ -127,7 +127,7 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
                      (const uint8_t*)R.rec_code.as<uint8_t>(), (const uint8_t*)R.rec_inf.as<uint8_t>(),
                      (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
                      (const uint32_t*)c->neg_g2.as<uint32_t>(), (const uint4*)R.pk_coeffs.as<uint4>(),
-                     R.rec_f.as<uint4>(), R.rec_f2.as<uint4>(), M, d_group, (uint64_t)R.K);
+                     R.rec_f.as<uint4>(), R.rec_f2.as<uint4>(), M, d_group, (uint64_t)R.K, (const uint8_t*)nullptr);
   hipLaunchKernelGGL(k_fp12_prod_segs, dim3((unsigned)NR), dim3((unsigned)kProdLanes), 0, s, (uint32_t)NR, d_tbeg,
                      (const uint4*)R.rec_f.as<uint4>(), (uint64_t)M, R.part2.as<uint4>(), R.acc.as<uint4>());
   HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));

@@ -20,7 +20,8 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
                                      const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
                                      const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
                                      uint4* __restrict__ pp, uint64_t stride,
-                                     const uint32_t* __restrict__ cidx, uint64_t cstride) {
+                                     const uint32_t* __restrict__ cidx, uint64_t cstride,
+                                     const uint8_t* __restrict__ cnorm) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (code[i] != 0) return;
@@ -37,6 +38,9 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
     return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
   };
   auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, cstride, cj, k) : ld_coeff_uniform(neg_g2, k); };
-  miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src);
+  // cnorm (keyed batches): the key's lines were normalised to c2 = 1
+  // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0
+  const bool norm1 = cnorm && cidx && cnorm[cj];
+  miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1);
   copy12(GlobF12{fout, stride, i}, f);
 }

@@ -204,6 +204,16 @@ int emu_g1_torsion_free(const uint32_t* x, const uint32_t* y, int rcb) {
   return rcb ? g1_is_torsion_free_rcb(px, py) : g1_is_torsion_free(px, py);
 }
 
+// emu_set_norm_pk(1): emu_verify normalises the key's lines to c2 = 1 with
+// normalize_lines (as k_norm_keys does for a distinct-key table) and runs the
+// Miller loop with norm1; returns the previous setting
+static int g_norm_pk = 0;
+int emu_set_norm_pk(int v) {
+  const int o = g_norm_pk;
+  g_norm_pk = v;
+  return o;
+}
+
 // full per-signature verification with the kernel algorithms; gt_out (576 B) optional
 int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint8_t* pk, uint8_t* gt_out) {
   init_neg_g2();
@@ -219,6 +229,12 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   fp2 qx = q.inf ? fp2{fp_from(c::G2_GEN_X0), fp_from(c::G2_GEN_X1)} : q.x;
   fp2 qy = q.inf ? fp2{fp_from(c::G2_GEN_Y0), fp_from(c::G2_GEN_Y1)} : q.y;
   g2_prepare(qx, qy, [](int i, const coeff3& k) { pkc[i] = k; });
+  bool norm1 = false;
+  if (g_norm_pk) {
+    static fp2 pre[N_COEFFS];
+    norm1 = normalize_lines([](int k) { return pkc[k]; }, [](int k, const coeff3& c) { pkc[k] = c; },
+                            [](int k) { return pre[k]; }, [](int k, const fp2& v) { pre[k] = v; });
+  }
   // the staged (store-based) Miller loop and final-exponentiation program the
   // kernels run, on plain-memory stores; the value-based versions in
   // pairing.hpp are kept as an independent cross-check (emu_gt_valuebased)
@@ -228,7 +244,7 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
   pts[0] = s;
   pts[1] = h;
   miller_loop2_staged(ArrF12{&slots[SL_F]}, !s.inf, !(q.inf || h.inf), [](int pair) { return pts[pair]; },
-                      [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
+                      [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; }, norm1);
   static fp12 park, acc1;
   const int which = final_exp_staged(ArrF12{&acc}, ArrF12{&acc1}, prog, [](int sl) { return ArrF12{&slots[sl]}; },
                                      ArrF12{&park});

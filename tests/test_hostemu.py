@@ -32,6 +32,24 @@ def test_codes_and_gt(emu, vectors):
             assert bytes(gt).hex() == c["gt"], c["name"]
 
 
+def test_normalized_key_lines_keep_gt(emu, vectors):
+    """A distinct-key table's lines scaled to c2 = 1 by normalize_lines (one
+    Fp2 inversion per key, k_norm_keys) and the Miller loop's norm1 path
+    (pair 1 through the 9-product sparse multiply) give the golden codes and
+    Gt bytes."""
+    old = emu.emu_set_norm_pk(1)
+    try:
+        for c in vectors["cases"]:
+            s, m, k = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+            gt = (ctypes.c_uint8 * 576)()
+            code = emu.emu_verify(s, m, len(m), k, gt)
+            assert code == c["code"], c["name"]
+            if "gt" in c:
+                assert bytes(gt).hex() == c["gt"], c["name"]
+    finally:
+        emu.emu_set_norm_pk(old)
+
+
 def test_hash_to_g1(emu, vectors):
     import oracle.bls_oracle as o
     for h in vectors["hash_to_g1"]:

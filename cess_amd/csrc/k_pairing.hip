@@ -31,8 +31,9 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   uint8_t fl = inf[i];
   __shared__ uint4 F[36][256];
   LdsF12 f{F, threadIdx.x};
-  // the G1 points are re-read from HBM (L2) for every line instead of being
-  // held in 48 registers across the loop
+  // the G1 points are re-read from HBM (L2) for every line: held in 48
+  // registers across the loop they cost spills (scratch 72 -> 320 B/lane,
+  // k_miller 163 -> 171 ms per 1 M, profiles/round3_h_sweep.txt)
   auto pt = [&](int pair) {
     const uint32_t* b = pair ? h_aff : sig_aff;
     return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};

@@ -402,8 +402,9 @@ def run_rsa(args, ctx, rank, world):
         verify_ms = ver_ms / ver_launches                  # average launch duration, HIP events
         achieved = n * RSA2048_ALG_MADS / (verify_ms * 1e-3)
         sha = lib_sha256()
-        pmc = load_pmc_traffic(sha, "k_rsa_verify_2048", n)
-        kd = (pmc or {}).get("all", {}).get("k_rsa_verify_2048", {})
+        # one key, many records: the key-uniform kernel (host_rsa.cpp policy)
+        pmc = load_pmc_traffic(sha, "k_rsa_verify_2048u", n)
+        kd = (pmc or {}).get("all", {}).get("k_rsa_verify_2048u", {})
         cpu = None
         if world == 1 and args.cpu_sample > 0:
             kn, ke = bls_rsa_key(key)
@@ -419,7 +420,7 @@ def run_rsa(args, ctx, rank, world):
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
             "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
-            "roofline": {"bound": "valu-int", "kernel": "k_rsa_verify_2048",
+            "roofline": {"bound": "valu-int", "kernel": "k_rsa_verify_2048u",
                          "achieved": achieved / 1e12, "peak": PEAK_MADS / 1e12,
                          "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)", "frac": achieved / PEAK_MADS,
                          "traffic": kd.get("hbm_bytes_per_launch"), "traffic_source": pmc["_file"] if pmc else None,

@@ -7,7 +7,8 @@
 // from_public_key_der; or PKCS#1 RSAPublicKey, the 270-byte Podr2Key of
 // primitives/common/src/lib.rs:54) and precomputes the Montgomery constants
 // (n in 28-bit limbs, -n^-1 mod 2^28, R^2 mod n); every signature is checked
-// on the GPU (k_rsa_classify + k_rsa_verify_{1024,2048}).
+// on the GPU (k_rsa_classify + k_rsa_verify_{1024,2048}; few-key batches:
+// k_rsa_count / _scan / _scatter + k_rsa_verify_2048u).
 #include "host.hpp"
 #include "rsa.hpp"
 
@@ -20,6 +21,17 @@ __global__ void k_rsa_classify(uint64_t, const uint32_t*, uint32_t, const RsaKey
                        const uint64_t*, const uint8_t*, const uint64_t*, uint32_t*, uint8_t*);
 RSA_KERNEL_DECL(k_rsa_verify_1024)
 RSA_KERNEL_DECL(k_rsa_verify_2048)
+RSA_KERNEL_DECL(k_rsa_verify_2048u)
+__global__ void k_rsa_count(uint64_t, const uint32_t*, uint32_t, const RsaKeyDev*, const uint8_t*, const uint64_t*,
+                            const uint64_t*, uint8_t*, uint32_t*);
+__global__ void k_rsa_scan(uint32_t, const uint32_t*, uint32_t*, uint32_t*);
+__global__ void k_rsa_scatter(uint64_t, const uint32_t*, uint32_t, const RsaKeyDev*, const uint8_t*, const uint64_t*,
+                              const uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint64_t);
+// key-uniform lists when the table has at most this many keys and the batch at
+// least this many records per key (padding each (class, key) segment to a
+// multiple of 64 then costs < 25 % idle lanes in the worst case)
+constexpr uint32_t kRsaUniformMaxKeys = 4096;
+constexpr uint64_t kRsaUniformMinPerKey = 256;
 
 namespace {
 
@@ -232,8 +244,44 @@ static int rsa_run(cess_bls_ctx* c, RsaTable& T, hipStream_t s, uint64_t n, cons
   if (n == 0) return CESS_BLS_OK;
   if (n >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
   RsaState& S = rsa_state(c);
-  if (S.lists.ensure(2 * n * 4) | S.counts.ensure(16) | S.base.ensure(n * RSA_LMAX * 4)) return CESS_BLS_E_OOM;
   if (T.keys.ensure(sizeof(RsaKeyDev)) | T.ok.ensure(1)) return CESS_BLS_E_OOM;
+  const RsaKeyDev* K = T.keys.as<RsaKeyDev>();
+  // Few keys with many records each (the TEE-key workload): key-sorted,
+  // wave-padded lists, so each wave of the 2048-bit kernel has one key and its
+  // modulus is a scalar operand (k_rsa_2048u).  Otherwise unsorted lists.
+  if (T.n > 0 && T.n <= kRsaUniformMaxKeys && n >= kRsaUniformMinPerKey * (uint64_t)T.n) {
+    const uint64_t nk = T.n, cap = n + 64 * nk;   // each (class, key) segment pads < 64 entries
+    if (S.lists.ensure(2 * cap * 4) | S.counts.ensure((6 * nk + 2) * 4) | S.base.ensure(cap * RSA_LMAX * 4))
+      return CESS_BLS_E_OOM;
+    uint32_t* cnt = S.counts.as<uint32_t>();
+    uint32_t *cur = cnt + 2 * nk, *segbase = cnt + 4 * nk, *totals = cnt + 6 * nk;
+    HIPCHK(hipMemsetAsync(cnt, 0, 4 * nk * 4, s));
+    HIPCHK(hipMemsetAsync(S.lists.p, 0xff, 2 * cap * 4, s));   // RSA_PAD
+    hipEvent_t a;
+    int r = prof_begin(c, s, ST_RSA_CLASSIFY, &a);
+    if (r) return r;
+    hipLaunchKernelGGL(k_rsa_count, dim3(grid_for(n)), dim3(kBlock), 0, s, n, d_idx, T.n, K,
+                       (const uint8_t*)T.ok.as<uint8_t>(), d_soffs, d_moffs, d_codes, cnt);
+    hipLaunchKernelGGL(k_rsa_scan, dim3(1), dim3(64), 0, s, T.n, (const uint32_t*)cnt, segbase, totals);
+    hipLaunchKernelGGL(k_rsa_scatter, dim3(grid_for(n)), dim3(kBlock), 0, s, n, d_idx, T.n, K,
+                       (const uint8_t*)T.ok.as<uint8_t>(), d_soffs, d_moffs, (const uint32_t*)segbase, cur,
+                       S.lists.as<uint32_t>(), cap);
+    r = prof_end(c, s, ST_RSA_CLASSIFY, a);
+    if (r) return r;
+    const uint32_t* L = S.lists.as<uint32_t>();
+    uint32_t* B = S.base.as<uint32_t>();
+    r = prof_begin(c, s, ST_RSA_VERIFY, &a);
+    if (r) return r;
+    hipLaunchKernelGGL(k_rsa_verify_2048u, dim3(grid_for(cap)), dim3(kBlock), 0, s, (uint32_t)cap,
+                       (const uint32_t*)(totals + 1), L + cap, d_idx, K, d_sigs, d_soffs, d_msgs, d_moffs, B, d_codes);
+    hipLaunchKernelGGL(k_rsa_verify_1024, dim3(grid_for(cap)), dim3(kBlock), 0, s, (uint32_t)cap,
+                       (const uint32_t*)totals, L, d_idx, K, d_sigs, d_soffs, d_msgs, d_moffs, B, d_codes);
+    r = prof_end(c, s, ST_RSA_VERIFY, a);
+    if (r) return r;
+    HIPCHK(hipGetLastError());
+    return CESS_BLS_OK;
+  }
+  if (S.lists.ensure(2 * n * 4) | S.counts.ensure(16) | S.base.ensure(n * RSA_LMAX * 4)) return CESS_BLS_E_OOM;
   HIPCHK(hipMemsetAsync(S.counts.p, 0, 16, s));
   // per-launch HIP events on s (CESS_BLS_F_PROFILE): bench.py's roofline
   // takes the verification kernel's duration from them
@@ -247,7 +295,6 @@ static int rsa_run(cess_bls_ctx* c, RsaTable& T, hipStream_t s, uint64_t n, cons
   if (r) return r;
   const uint32_t* cnt = S.counts.as<uint32_t>();
   const uint32_t* L = S.lists.as<uint32_t>();
-  const RsaKeyDev* K = T.keys.as<RsaKeyDev>();
   uint32_t* B = S.base.as<uint32_t>();
   // every class kernel covers n lanes; lanes past the class's count exit
   r = prof_begin(c, s, ST_RSA_VERIFY, &a);

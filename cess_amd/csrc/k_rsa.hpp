@@ -143,7 +143,11 @@ using namespace rsa_detail;
 // the distinct-key table (rsa.hpp RsaKeyDev).  base: SoA scratch (L words per
 // lane, stride `cnt` = the launch's n_max) for s R mod n, re-read for the final multiply of each
 // exponent bit, so the exponentiation keeps 3 L values live (x, n, m).
-template <int L>
+// UNI: the wave's records share one key (key-sorted, wave-padded lists of
+// k_rsa_scatter), so the key row is read through a wave-uniform index and the
+// modulus limbs live in SGPRs: the exponentiation keeps 2 L values (x, m) in
+// VGPRs instead of 3 L.  PAD list entries (0xffffffff) are inactive lanes.
+template <int L, bool UNI = false>
 __device__ __forceinline__ void rsa_verify_lane(uint32_t t, uint32_t cnt, const uint32_t* __restrict__ rec,
                                                 const uint32_t* __restrict__ key_idx,
                                                 const RsaKeyDev* __restrict__ keys, const uint8_t* __restrict__ sigs,
@@ -151,7 +155,9 @@ __device__ __forceinline__ void rsa_verify_lane(uint32_t t, uint32_t cnt, const 
                                                 const uint64_t* __restrict__ msg_offs, uint32_t* __restrict__ base,
                                                 uint8_t* __restrict__ codes) {
   const uint32_t r = rec[t];
-  const RsaKeyDev& K = keys[key_idx[r]];
+  if (r == RSA_PAD) return;
+  const uint32_t ki = key_idx[r];
+  const RsaKeyDev& K = keys[UNI ? __builtin_amdgcn_readfirstlane(ki) : ki];
   const int kb = (int)K.k_bytes;
   uint32_t n[L], x[L];
 #pragma unroll
@@ -241,7 +247,7 @@ __device__ __forceinline__ void rsa_verify_lane(uint32_t t, uint32_t cnt, const 
 }
 
 // rec: this class's record list (its length at *cnt, filled by
-// k_rsa_classify); base: SoA scratch of stride n_max.
+// k_rsa_classify or k_rsa_scatter); base: SoA scratch of stride n_max.
 #define CESS_RSA_KERNEL(NAME, L, WAVES)                                                                              \
   __global__ __launch_bounds__(256, WAVES) void NAME(                                                                \
       uint32_t n_max, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ rec,                            \
@@ -251,4 +257,14 @@ __device__ __forceinline__ void rsa_verify_lane(uint32_t t, uint32_t cnt, const 
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;                                                        \
     if (t >= *cnt) return;                                                                                           \
     rsa_verify_lane<L>(t, n_max, rec, key_idx, keys, sigs, sig_offs, msgs, msg_offs, base, codes);                  \
+  }
+#define CESS_RSA_KERNEL_U(NAME, L, WAVES)                                                                            \
+  __global__ __launch_bounds__(256, WAVES) void NAME(                                                                \
+      uint32_t n_max, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ rec,                            \
+      const uint32_t* __restrict__ key_idx, const RsaKeyDev* __restrict__ keys, const uint8_t* __restrict__ sigs,   \
+      const uint64_t* __restrict__ sig_offs, const uint8_t* __restrict__ msgs,                                      \
+      const uint64_t* __restrict__ msg_offs, uint32_t* __restrict__ base, uint8_t* __restrict__ codes) {            \
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;                                                        \
+    if (t >= *cnt) return;                                                                                           \
+    rsa_verify_lane<L, true>(t, n_max, rec, key_idx, keys, sigs, sig_offs, msgs, msg_offs, base, codes);            \
   }

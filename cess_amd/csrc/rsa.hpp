@@ -10,6 +10,9 @@
 #define RSA_L2048 74
 #define RSA_LMAX RSA_L2048
 
+// an inactive entry of a wave-padded record list (k_rsa_scatter)
+#define RSA_PAD 0xffffffffu
+
 // verdict codes (oracle/rsa_oracle.py)
 enum : uint8_t { RSA_OK = 0, RSA_SIG_LEN = 1, RSA_SIG_RANGE = 2, RSA_MSG_LEN = 3, RSA_MISMATCH = 4, RSA_KEY = 5 };
 

@@ -143,15 +143,19 @@ def encode_spki(n: int, e: int) -> bytes:
 
 
 # --- verify (rsa 0.8.2 pkcs1v15 verify with Pkcs1v15Sign::new_raw()) ----------
+# The crate answers every failure below with Error::Verification (verify_rsa:
+# false); the distinct codes are this build's refinement, in the precedence the
+# GPU path applies them: lengths first (k_rsa_classify), then the range and the
+# encoded message (k_rsa_verify_*).
 def verify_code(n: int, e: int, msg: bytes, sig: bytes) -> int:
     k = (n.bit_length() + 7) // 8
     if len(sig) != k:
         return SIG_LEN
+    if k < len(msg) + 11:
+        return MSG_LEN
     s = int.from_bytes(sig, "big")
     if s >= n:
         return SIG_RANGE
-    if k < len(msg) + 11:
-        return MSG_LEN
     em = pow(s, e, n).to_bytes(k, "big")
     want = b"\x00\x01" + b"\xff" * (k - len(msg) - 3) + b"\x00" + msg
     return OK if em == want else MISMATCH

@@ -56,6 +56,7 @@ def main():
         add(f"k{ki}_sig_zero", ki, hw, bytes(kb))
         add(f"k{ki}_sig_one", ki, b"", (1).to_bytes(kb, "big"))
         add(f"k{ki}_msg_too_long", ki, bytes(kb - 10), s)
+        add(f"k{ki}_msg_too_long_sig_max", ki, bytes(kb - 10), b"\xff" * kb)   # length code first
         # wrong block type (0x02) and a missing separator, both validly exponentiated
         for nm, em in (("bt02", b"\x00\x02" + b"\xff" * (kb - len(hw) - 3) + b"\x00" + hw),
                        ("nosep", b"\x00\x01" + b"\xff" * (kb - len(hw) - 2) + hw),

@@ -10,7 +10,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 sha256sum cess_amd/lib/libcess_bls.so > $OUT/lib_sha256.txt
 export TMPDIR=/tmp
-RX="k_rsa_verify_2048|k_rsa_classify"
+RX="k_rsa_verify_2048|k_rsa_classify|k_rsa_count|k_rsa_scatter"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --mode rsa --n $N --steps 3 --warmup 1 --cpu-sample 0 > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail -20 $OUT/trace.log; exit 1; }
 echo "trace ok"
 i=0

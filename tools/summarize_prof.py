@@ -27,7 +27,8 @@ if stats:
 agg = {}
 for f in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if int(r["Grid_Size"]) != n:
+        # (grid = n, or n plus the padding of a wave-padded list: k_rsa_verify_2048u)
+        if not n <= int(r["Grid_Size"]) <= n + (1 << 18):
             continue
         k = r["Kernel_Name"].split("(")[0]
         d = agg.setdefault(k, {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),

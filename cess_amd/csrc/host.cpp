@@ -589,7 +589,7 @@ int cess_keys_load_one(cess_bls_ctx* c, size_t k, const uint8_t* pks, uint8_t* k
                      c->key_code.as<uint8_t>(), (const uint8_t*)c->key_inf.as<uint8_t>());
   // every signature of a key reuses its lines: normalise them once (the
   // keyed Miller loop then costs 9 Fp2 products per key line instead of 13)
-  hipLaunchKernelGGL(k_norm_keys, dim3(grid_for(k)), dim3(kBlock), 0, s, (uint64_t)k, c->key_coeffs.as<uint4>(),
+  hipLaunchKernelGGL(k_norm_keys, dim3(grid_for(k)), dim3(kBlock), 0, s, (uint64_t)k, (uint64_t)k, c->key_coeffs.as<uint4>(),
                      pre.as<uint32_t>(), c->key_norm.as<uint8_t>());
   HIPCHK(hipGetLastError());
   if (key_codes_out) HIPCHK(hipMemcpyAsync(key_codes_out, c->key_code.p, k, hipMemcpyDeviceToHost, s));

@@ -40,8 +40,10 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   };
   auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, cstride, cj, k) : ld_coeff_uniform(neg_g2, k); };
   // cnorm (keyed batches): the key's lines were normalised to c2 = 1
-  // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0
-  const bool norm1 = cnorm && cidx && cnorm[cj];
+  // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0.
+  // (Per-signature rows are not normalised: k_norm_keys over every record
+  // costs 22 ms per 1 M against 18 ms saved here, profiles/round3_k_sweep.txt.)
+  const bool norm1 = cnorm && cnorm[cj];
   miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1);
   copy12(GlobF12{fout, stride, i}, f);
 }

@@ -48,13 +48,13 @@ __global__ __launch_bounds__(128) void k_norm_lines(uint4* __restrict__ tab) {
 // (pairing.hpp normalize_lines: one Fp2 inversion per key), once per
 // cess_bls_keys_load, so the keyed Miller loop multiplies pair 1 by
 // normalised lines as well (9 Fp2 products per line instead of 13).  tab:
-// k_prepare's uint4-row table (stride K); pre: 68 Fp2 of scratch per key
-// (word-SoA, stride K); norm[i] = 1 if key i was normalised, 0 if a zero c2
-// kept its lines as they were.
-__global__ CESS_LB void k_norm_keys(uint64_t K, uint4* __restrict__ tab, uint32_t* __restrict__ pre,
+// k_prepare's uint4-row table (n rows of stride K); pre: 68 Fp2 of scratch
+// per key (word-SoA, stride K); norm[i] = 1 if key i was normalised, 0 if a
+// zero c2 kept its lines as they were.
+__global__ CESS_LB void k_norm_keys(uint64_t n, uint64_t K, uint4* __restrict__ tab, uint32_t* __restrict__ pre,
                                     uint8_t* __restrict__ norm) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= K) return;
+  if (i >= n) return;
   const bool ok = normalize_lines([&](int k) { return ld_coeff4(tab, K, i, k); },
                                   [&](int k, const coeff3& c) { st_coeff4(tab, K, i, k, c); },
                                   [&](int k) { return ld_fp2(pre + (uint64_t)(24 * k) * K, K, i); },

@@ -66,11 +66,12 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=40960, help="records for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
-    ap.add_argument("--mode", choices=["persig", "rlc", "adversarial", "keyed", "rsa"], default="persig",
+    ap.add_argument("--mode", choices=["persig", "rlc", "adversarial", "keyed", "rsa", "sign"], default="persig",
                     help="persig: BASELINE config[1]/[2] (default); rlc: config[3] shape (few keys, RLC batch "
                          "mode + Gt-partial all-gather); adversarial: config[4] shape (1%% invalid mix, exact codes); "
                          "keyed: config[3] shape with per-signature verdicts; rsa: SURVEY §8(f) rank 4, RSA-2048 "
-                         "PKCS#1 v1.5 raw verify (cp_enclave_verify::verify_rsa) over 32-byte messages")
+                         "PKCS#1 v1.5 raw verify (cp_enclave_verify::verify_rsa) over 32-byte messages; sign: SURVEY §8(f) "
+                         "rank 3, batch PrivateKey::sign")
     ap.add_argument("--keys", type=int, default=16, help="distinct keys (rlc / keyed modes)")
     ap.add_argument("--forged-count", type=int, default=0, help="forgeries per rank (rlc mode)")
     ap.add_argument("--dry-run", action="store_true",
@@ -446,6 +447,81 @@ def bls_rsa_key(der):
 # ---------------------------------------------------------------------------
 # rank body
 # ---------------------------------------------------------------------------
+def run_sign(args, ctx, rank, world):
+    """SURVEY §8(f) rank 3: the TEE side's batch signer, PrivateKey::sign
+    (src/lib.rs:233-236) = compress([sk] H(m)), n records resident in HBM
+    (cess_bls_sign_batch_device, one k_sign launch per step).  Untimed check:
+    every signature verifies against its key (cess_bls_verify_batch_device)."""
+    import numpy as np
+    n = args.n or N1_DEFAULT
+    rng = np.random.default_rng((0x5167, rank))
+    sk = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sk[:, 0] &= 0x3F                                   # < 2^254 < r
+    M = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    d_sk = ctx.to_device(sk)
+    d_msg = ctx.to_device(M)
+    d_off = ctx.to_device(np.arange(n + 1, dtype=np.uint64) * 32)
+    d_sig = ctx.device_alloc(48 * n)
+
+    def step():
+        ctx.sign_device(n, d_sk, d_msg, d_off, d_sig)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    if world > 1:
+        ctx.comm_barrier()
+    ctx.stage_stats(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    if world > 1:
+        ctx.comm_barrier()
+    elapsed = time.perf_counter() - t0
+    st = {k: v for k, v in ctx.stage_stats(reset=True).items() if v[1] > 0}
+    # untimed: the signatures verify against keys from the keygen kernel
+    pks = ctx.public_keys_raw(sk.tobytes())
+    d_pk = ctx.to_device(np.frombuffer(pks, dtype=np.uint8))
+    d_codes = ctx.device_alloc(n)
+    d_bm = ctx.device_alloc(8 * ((n + 63) // 64))
+    ctx.verify_device(n, d_sig, d_pk, d_msg, d_off, d_codes, d_bm)
+    ctx.synchronize()
+    ok = bool((np.frombuffer(ctx.from_device(d_codes, n), dtype=np.uint8) == 0).all())
+    if world > 1:
+        elapsed = ctx.comm_max(elapsed)
+        ok = ctx.comm_max(0.0 if ok else 1.0) == 0.0
+    if rank == 0:
+        value = n * world * args.steps / elapsed
+        sign_ms, launches = st["k_sign"]
+        assert launches == args.steps, st
+        with open(os.path.join(ROOT, "profiles", "opcount.json")) as f:
+            g = json.load(f)["generator"]["k_sign"]
+        alg = (g["mul"] + g["sqr"]) * ALG_MADS_PER_FP_MUL
+        achieved = n * alg / (sign_ms / launches * 1e-3)
+        print(json.dumps({
+            "metric": "BLS12-381 signatures produced/sec (PrivateKey::sign)", "value": value, "unit": "sigs/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32 (381-bit Montgomery, 14x28-bit limb products via v_mad_u64_u32)",
+            "data": "synthetic: random secret keys < 2^254 and 32-byte messages, inputs in HBM",
+            "config": {"workload": f"SURVEY §8(f) rank 3, batch PrivateKey::sign: {n} records per GPU",
+                       "parallelism": f"shard-by-index x{world}"},
+            "verdicts_ok": ok,
+            "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
+            "roofline": {"bound": "valu-int", "kernel": "k_sign", "achieved": achieved / 1e12,
+                         "peak": PEAK_MADS / 1e12, "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
+                         "frac": achieved / PEAK_MADS, "traffic": None,
+                         "alg_mads_per_sig": alg,
+                         "note": "achieved = algorithmic mads of one launch (profiles/opcount.json generator.k_sign "
+                                 "x 288) / its HIP-event duration"},
+            "cpu_baseline": None,
+            "runtime": dict(runtime_provenance(), lib_sha256=lib_sha256()),
+        }), flush=True)
+    for d in (d_sk, d_msg, d_off, d_sig, d_pk, d_codes, d_bm):
+        ctx.device_free(d)
+
+
 def run_dry(args, rank, world):
     """CPU rehearsal of the N>1 path: rendezvous of a 128-byte id through the
     launcher's job directory, then the shard ranges of the config[2] batch from
@@ -559,6 +635,13 @@ def main():
         if world > 1:
             comm_setup(ctx, rank, world, args.transport)
         run_rsa(args, ctx, rank, world)
+        ctx.close()
+        return
+    if args.mode == "sign":
+        ctx = bls.Context(device=local, max_batch=min(n, 1 << 20), profile=True)
+        if world > 1:
+            comm_setup(ctx, rank, world, args.transport)
+        run_sign(args, ctx, rank, world)
         ctx.close()
         return
     if args.mode == "rlc":

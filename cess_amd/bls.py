@@ -36,7 +36,7 @@ CODE_NAMES = {0: "OK", 1: "SIG_LEN", 2: "SIG_POINT", 3: "PK_LEN", 4: "PK_POINT",
 EXPORTS = (
     "cess_bls_ctx_create", "cess_bls_ctx_destroy", "cess_bls_verify", "cess_bls_verify_batch",
     "cess_bls_verify_batch_var", "cess_bls_verify_batch_device", "cess_bls_public_key_batch",
-    "cess_bls_sign_batch", "cess_bls_hash_to_g1_batch", "cess_bls_gt_batch", "cess_bls_stage_times",
+    "cess_bls_sign_batch", "cess_bls_sign_batch_device", "cess_bls_hash_to_g1_batch", "cess_bls_gt_batch", "cess_bls_stage_times",
     "cess_bls_status_string", "cess_bls_version",
     "cess_bls_verify_batch_rlc", "cess_bls_rlc_begin", "cess_bls_gt_product_is_one", "cess_bls_rlc_finish",
     "cess_bls_keys_load", "cess_bls_verify_batch_keyed", "cess_bls_verify_batch_keyed_device",
@@ -113,6 +113,7 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_verify_batch_keyed_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
         lib.cess_bls_public_key_batch.argtypes = [vp, sz, _u8p, _u8p]
         lib.cess_bls_sign_batch.argtypes = [vp, sz, _u8p, _u8p, _u64p, _u8p]
+        lib.cess_bls_sign_batch_device.argtypes = [vp, sz, vp, vp, vp, vp, vp]
         lib.cess_bls_hash_to_g1_batch.argtypes = [vp, sz, _u8p, _u64p, _u8p]
         lib.cess_bls_gt_batch.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p]
         lib.cess_bls_rlc_begin.argtypes = [vp, sz, _u8p, _u8p, _u8p, _u64p, _u8p, _u8p]
@@ -284,6 +285,11 @@ class Context:
                                               _offsets([len(r[1]) for r in records]), codes, gt))
         raw = bytes(gt)
         return bytes(codes), [raw[576 * i:576 * (i + 1)] for i in range(n)]
+
+    def sign_device(self, n, d_sks, d_msgs, d_offs, d_sigs_out, stream=0):
+        """cess_bls_sign_batch_device: enqueue PrivateKey::sign over device buffers."""
+        self._chk(self._lib.cess_bls_sign_batch_device(self._h, n, d_sks, d_msgs, d_offs, d_sigs_out,
+                                                       stream or None))
 
     def verify_device(self, n, d_sigs, d_pks, d_msgs, d_offs, d_codes, d_bitmap, stream=0):
         """Device-resident batch (HBM pointers as ints); enqueued on `stream`, not synchronised."""

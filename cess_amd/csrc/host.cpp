@@ -16,7 +16,7 @@ using namespace cess_host;
 
 namespace {
 const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk",    "k_hash",       "k_prepare", "k_miller",
-                                 "k_final",      "k_rsa_classify", "k_rsa_verify", "k_group"};
+                                 "k_final",      "k_rsa_classify", "k_rsa_verify", "k_group",  "k_sign"};
 }
 
 extern "C" const char* cess_bls_version(void) { return "cess_amd-bls 0.2 (gfx950)"; }
@@ -775,6 +775,27 @@ extern "C" int cess_bls_sign_batch(cess_bls_ctx* c, size_t n, const uint8_t* sks
   if ((!sks || !offs) && n) return CESS_BLS_E_INVALID_ARG;
   return gen_batch(c, 1, n, sks, msgs, offs, sigs_out);
 }
+// PrivateKey::sign over device-resident records (the TEE-side batch signer,
+// SURVEY §8(f) rank 3): one k_sign launch, enqueued on `stream`.
+extern "C" int cess_bls_sign_batch_device(cess_bls_ctx* c, size_t n, const uint8_t* d_sks, const uint8_t* d_msgs,
+                                          const uint64_t* d_offs, uint8_t* d_sigs_out, void* stream) {
+  ENTRY(c);
+  if (!c->subs.empty() || (n && (!d_sks || !d_offs || !d_sigs_out))) return CESS_BLS_E_INVALID_ARG;
+  if (n == 0) return CESS_BLS_OK;
+  if (n >= (1ull << 40)) return CESS_BLS_E_INVALID_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  int r = order_begin(c, s);
+  if (r) return r;
+  LAUNCH(ST_SIGN, s, k_sign, dim3(grid_for(n)), dim3(kBlock), 0, s, (uint64_t)n, d_sks, d_msgs, d_offs, d_sigs_out);
+  HIPCHK(hipGetLastError());
+  if (c->flags & CESS_BLS_F_PROFILE) {
+    r = collect_profile(c, s);
+    if (r) return r;
+  }
+  return order_end(c, s);
+}
+
 extern "C" int cess_bls_hash_to_g1_batch(cess_bls_ctx* c, size_t n, const uint8_t* msgs, const uint64_t* offs,
                                          uint8_t* out48) {
   ENTRY(c);

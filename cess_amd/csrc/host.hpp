@@ -47,7 +47,7 @@ __global__ void k_fp12_prod_segs(uint32_t, const uint32_t*, const uint4*, uint64
 namespace cess_host {
 
 enum Stage { ST_DECODE_SIG, ST_DECODE_PK, ST_HASH, ST_PREPARE, ST_MILLER, ST_FINAL, ST_RSA_CLASSIFY, ST_RSA_VERIFY,
-             ST_GROUP, ST_N };
+             ST_GROUP, ST_SIGN, ST_N };
 constexpr int kBlock = 256;
 
 inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }

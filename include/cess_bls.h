@@ -157,6 +157,12 @@ int cess_bls_public_key_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* sks, u
 int cess_bls_sign_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* sks, const uint8_t* msgs,
                         const uint64_t* msg_offsets, uint8_t* sigs_out);
 
+/* cess_bls_sign_batch over device buffers (d_sks: n * 32 B, d_msgs with n + 1
+ * offsets, d_sigs_out: n * 48 B), enqueued on `stream` (null: the context's)
+ * without waiting: the batch signer of the TEE side. */
+int cess_bls_sign_batch_device(cess_bls_ctx* ctx, size_t n, const uint8_t* d_sks, const uint8_t* d_msgs,
+                               const uint64_t* d_msg_offsets, uint8_t* d_sigs_out, void* stream);
+
 /* hash_to_g1 (src/lib.rs:25-31), compressed 48-byte output; exposed for tests. */
 int cess_bls_hash_to_g1_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* msgs, const uint64_t* msg_offsets,
                               uint8_t* out48);

@@ -150,6 +150,23 @@ void emu_opcount(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const ui
                          ArrF12{&park});
   snap(5);
 }
+
+// (mul, sqr) counts of k_sign's body for one record (PrivateKey::sign,
+// src/lib.rs:233-236): hash_to_g1, [sk] H(m), affine conversion, compression
+void emu_opcount_sign(const uint8_t* sk, const uint8_t* msg, uint32_t mlen, uint64_t* out) {
+  uint32_t k[8];
+  for (int w = 0; w < 8; w++) {
+    const uint8_t* q = sk + 28 - 4 * w;
+    k[w] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  g_mul_count = g_sqr_count = g_mul2_count = g_half_count = 0;
+  g1a h = hash_to_g1(msg, mlen);
+  g1a s = proj_to_affine(proj_mul_scalar_mixed(h.x, h.y, k));
+  uint8_t b[48];
+  g1_compress(s, b);
+  out[0] = 2 * g_mul_count + 5 * g_mul2_count + g_half_count;   // half-multiplies
+  out[1] = g_sqr_count;
+}
 #endif
 
 // 1 if the two-wave ping-pong Miller loop (miller2.hpp) gives the same Fp12 as

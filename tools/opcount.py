@@ -35,6 +35,15 @@ res = {
     "algorithmic_mads_per_sig": (tot_m + tot_s) * 288,
     "issued_mads_per_sig": tot_m * 392 + tot_s * 301,
 }
+# generator side: k_sign (PrivateKey::sign) over the golden keygen/sign records
+srows = []
+for g in vec["keygen_sign"]:
+    out = (ctypes.c_uint64 * 2)()
+    m = bytes.fromhex(g["msg"])
+    L.emu_opcount_sign(bytes.fromhex(g["sk"]), m, len(m), out)
+    srows.append((out[0] / 2, out[1]))
+res["generator"] = {"k_sign": {"mul": sum(r[0] for r in srows) / len(srows),
+                               "sqr": sum(r[1] for r in srows) / len(srows), "samples": len(srows)}}
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 json.dump(res, open(os.path.join(ROOT, "profiles", "opcount.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -86,6 +86,8 @@ extern "C" {
     pub fn cess_bls_public_key_batch(ctx: *mut cess_bls_ctx, n: usize, sks: *const u8, pks_out: *mut u8) -> c_int;
     pub fn cess_bls_sign_batch(ctx: *mut cess_bls_ctx, n: usize, sks: *const u8, msgs: *const u8,
                                msg_offsets: *const u64, sigs_out: *mut u8) -> c_int;
+    pub fn cess_bls_sign_batch_device(ctx: *mut cess_bls_ctx, n: usize, d_sks: *const u8, d_msgs: *const u8,
+                                      d_msg_offsets: *const u64, d_sigs_out: *mut u8, stream: *mut c_void) -> c_int;
     pub fn cess_bls_hash_to_g1_batch(ctx: *mut cess_bls_ctx, n: usize, msgs: *const u8, msg_offsets: *const u64,
                                      out48: *mut u8) -> c_int;
     pub fn cess_bls_gt_batch(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8, msgs: *const u8,

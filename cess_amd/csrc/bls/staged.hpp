@@ -25,12 +25,29 @@
 namespace bls {
 
 #if !defined(CESS_HOSTEMU)
+// The lane's id within its wave, recomputed at every call (v_mbcnt_lo/hi in a
+// volatile asm, so LLVM can neither merge two calls nor hoist one): the
+// per-lane part of a store address then lives for one access only.  With the
+// address kept in a register for the whole kernel, k_miller's allocator
+// spilled it and reloaded it from scratch -- one serialised scratch round trip
+// (s_waitcnt vmcnt(0)) in front of every LDS access, ~110 per Miller step --
+// and k_final did the same with the 64-bit HBM slot addresses.
+CESS_HD uint32_t lane_fresh() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+// first thread (block-relative) of the calling lane's wave, wave-uniform (SGPR)
+CESS_HD uint32_t wave_first_thread() { return __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u); }
+
 // One lane's Fp12 in an LDS image F[36][256] (uint4 rows; lane t owns column t,
 // so a wave reads 16 consecutive bytes per lane: conflict-free ds_read_b128).
+// t = w0 + lane_fresh(): w0 is the wave's first thread (uniform).
 struct LdsF12 {
   uint4 (*F)[256];
-  uint32_t t;
+  uint32_t w0;
   CESS_HD fp2 ld(int k) const {
+    const uint32_t t = w0 + lane_fresh();
     fp2 r;
 #pragma unroll
     for (int q = 0; q < 6; q++) {
@@ -42,11 +59,44 @@ struct LdsF12 {
     return r;
   }
   CESS_HD void st(int k, const fp2& a) const {
+    const uint32_t t = w0 + lane_fresh();
 #pragma unroll
     for (int q = 0; q < 6; q++) {
       const fp& s = q < 3 ? a.c0 : a.c1;
       const int o = 4 * (q % 3);
       F[6 * k + q][t] = make_uint4(s.v[o], s.v[o + 1], s.v[o + 2], s.v[o + 3]);
+    }
+  }
+};
+
+// One lane's Fp12 in an HBM slot, addressed like LdsF12: `base` already points
+// at the wave's first lane (uniform), the lane id is recomputed per access
+// (k_final: scratch 2,012 -> 800 B/lane, 158.0 -> 147.0 ms per 1 M,
+// profiles/round3_n_sweep.txt).  (Uniform row bases + a 32-bit lane byte
+// offset, global_load voffset s[base], measured no better: 147.8 ms.)
+struct GlobF12W {
+  uint4* base;
+  uint64_t stride;
+  CESS_HD fp2 ld(int k) const {
+    const uint32_t l = lane_fresh();
+    fp2 r;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      uint4 x = base[(uint64_t)(6 * k + q) * stride + l];
+      fp& d = q < 3 ? r.c0 : r.c1;
+      const int o = 4 * (q % 3);
+      d.v[o] = x.x, d.v[o + 1] = x.y, d.v[o + 2] = x.z, d.v[o + 3] = x.w;
+    }
+    return r;
+  }
+  CESS_HD void st(int k, const fp2& a) const {
+    const uint32_t l = lane_fresh();
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const fp& s = q < 3 ? a.c0 : a.c1;
+      const int o = 4 * (q % 3);
+      const uint4 v = make_uint4(s.v[o], s.v[o + 1], s.v[o + 2], s.v[o + 3]);
+      base[(uint64_t)(6 * k + q) * stride + l] = v;
     }
   }
 };

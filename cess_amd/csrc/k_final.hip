@@ -26,16 +26,19 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
   if (i < n) {
     c = code[i];
     if (c == 0) {
-      // two HBM accumulators (slots SL_N - 1 and SL_N): FE_MUL ping-pongs
-      GlobF12 acc0{slots + (uint64_t)(SL_N - 1) * 36 * stride, stride, i};
-      GlobF12 acc1{slots + (uint64_t)SL_N * 36 * stride, stride, i};
+      // two HBM accumulators (slots SL_N - 1 and SL_N): FE_MUL ping-pongs.
+      // Slot views start at the wave's first record (uniform) and add the
+      // lane id per access (staged.hpp GlobF12W).
+      const uint32_t w0 = blockIdx.x * blockDim.x + wave_first_thread();
+      GlobF12W acc0{slots + (uint64_t)(SL_N - 1) * 36 * stride + w0, stride};
+      GlobF12W acc1{slots + (uint64_t)SL_N * 36 * stride + w0, stride};
       // 18 uint4 rows x 256 lanes = 72 KiB per block: two blocks per CU
       __shared__ uint4 park[18][256];
       const int which = final_exp_staged(
           acc0, acc1, kFeProgram,
-          [&](int s) { return GlobF12{s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride, stride, i}; },
-          LdsF12{park, threadIdx.x});
-      const GlobF12 acc = which ? acc1 : acc0;
+          [&](int s) { return GlobF12W{(s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride) + w0, stride}; },
+          LdsF12{park, wave_first_thread()});
+      const GlobF12W acc = which ? acc1 : acc0;
       if (!is_one12(acc)) c = CODE_PAIRING;
       if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
 #pragma unroll 1

@@ -30,10 +30,14 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   const uint32_t cj = cidx ? cidx[i] : i;
   uint8_t fl = inf[i];
   __shared__ uint4 F[36][256];
-  LdsF12 f{F, threadIdx.x};
+  LdsF12 f{F, wave_first_thread()};
   // the G1 points are re-read from HBM (L2) for every line: held in 48
   // registers across the loop they cost spills (scratch 72 -> 320 B/lane,
-  // k_miller 163 -> 171 ms per 1 M, profiles/round3_h_sweep.txt)
+  // k_miller 163 -> 171 ms per 1 M, profiles/round3_h_sweep.txt); with the
+  // lane-fresh LDS addressing (no scratch at all) the two forms run the same
+  // (156.6 vs 156.3 ms, profiles/round3_n_sweep.txt).  Row addresses formed
+  // as a uniform base + a 32-bit lane byte offset (global_load voffset,
+  // s[base]) measured slower (159.2 ms).
   auto pt = [&](int pair) {
     const uint32_t* b = pair ? h_aff : sig_aff;
     return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256, 1) void k_probe(int op, int iters, uint4* __re
                                                   uint32_t* __restrict__ sink) {
   __shared__ uint4 F[36][256];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  LdsF12 f{F, threadIdx.x};
+  LdsF12 f{F, wave_first_thread()};
   GlobF12 g{slot, stride, i};
   copy12(f, g);
   if (op == OP_FPMUL) {
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256, 1) void k_probe_ref(int op, int iters, uint4* 
                                                        uint4* __restrict__ out) {
   __shared__ uint4 F[36][256];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  LdsF12 f{F, threadIdx.x};
+  LdsF12 f{F, wave_first_thread()};
   GlobF12 g{slot, stride, i};
   copy12(f, g);
   if (op == OP_CYCSQ) {

@@ -170,6 +170,15 @@ CESS_HD bool is_one12(const S& s) {
   return r;
 }
 
+// a == conj(b), i.e. a b == 1 for b in the cyclotomic subgroup
+template <class A, class B>
+CESS_HD bool is_conj12(const A& a, const B& b) {
+  bool r = true;
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r = r && eq(a.ld(k), k < 3 ? b.ld(k) : neg(b.ld(k)));
+  return r;
+}
+
 // f <- f^2  (complex squaring: 2 Fp6 multiplies)
 template <class S>
 CESS_HD void sqr12(const S& f) {
@@ -378,7 +387,7 @@ enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6
 
 // easy part: m = f^((p^6 - 1)(p^2 + 1)); hard part as in pairing.hpp
 // final_exponentiation (t2 = m).  SL_T0 doubles as scratch in the easy part.
-#define CESS_FE_PROGRAM                                                                                           \
+#define CESS_FE_BODY                                                                                              \
   {FE_LOAD, SL_F}, {FE_CONJ, 0}, {FE_STORE, SL_T0}, {FE_LOAD, SL_F}, {FE_INV, 0}, {FE_MUL, SL_T0},                 \
       {FE_STORE, SL_T0}, {FE_FROB, 2}, {FE_MUL, SL_T0}, {FE_STORE, SL_M},                                          \
       /* t1 = conj(cycsq(m)) */ {FE_SQN, 1}, {FE_CONJ, 0}, {FE_STORE, SL_T1},                                     \
@@ -395,7 +404,12 @@ enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6
       /* t6 = frob1(t6 * conj(m)) */ {FE_LOAD, SL_M}, {FE_CONJ, 0}, {FE_MUL, SL_T6}, {FE_FROB, 1},              \
       {FE_STORE, SL_T6},                                                                                           \
       /* t3 = frob2(t3 * t0) * t1 * t6 * t4 */ {FE_LOAD, SL_T3}, {FE_MUL, SL_T0}, {FE_FROB, 2}, {FE_MUL, SL_T1},  \
-      {FE_MUL, SL_T6}, {FE_MUL, SL_T4}, {FE_END, 0}
+      {FE_MUL, SL_T6}
+#define CESS_FE_PROGRAM CESS_FE_BODY, {FE_MUL, SL_T4}, {FE_END, 0}
+// Verdict-only form (no Gt output): the result t3 * t4 is 1 iff t3 equals
+// t4^-1 = conj(t4) (t4 is in the cyclotomic subgroup), so the last multiply
+// becomes a comparison (is_conj12 of the accumulator and slot SL_T4).
+#define CESS_FE_PROGRAM_VERIFY CESS_FE_BODY, {FE_END, 0}
 
 // n cyclotomic squarings of acc (Granger-Scott formulas, as cyclotomic_square
 // in field.hpp): pair (z0, z1) updates itself; the square of (z2, z3) updates

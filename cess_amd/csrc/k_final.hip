@@ -13,6 +13,8 @@ using namespace bls;
 using namespace cess;
 
 __constant__ uint8_t kFeProgram[][2] = {CESS_FE_PROGRAM};
+// verdict only (no Gt bytes requested): one Fp12 multiply less (staged.hpp)
+__constant__ uint8_t kFeProgramVerify[][2] = {CESS_FE_PROGRAM_VERIFY};
 
 // two waves per SIMD (one wave with 512 registers and no scratch measured
 // slower: 245 vs 212 ms per 1 M, profiles/r02g_sweep.txt)
@@ -34,12 +36,13 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
       GlobF12W acc1{slots + (uint64_t)SL_N * 36 * stride + w0, stride};
       // 18 uint4 rows x 256 lanes = 72 KiB per block: two blocks per CU
       __shared__ uint4 park[18][256];
-      const int which = final_exp_staged(
-          acc0, acc1, kFeProgram,
-          [&](int s) { return GlobF12W{(s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride) + w0, stride}; },
-          LdsF12{park, wave_first_thread()});
+      auto slot = [&](int s) {
+        return GlobF12W{(s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride) + w0, stride};
+      };
+      const int which = final_exp_staged(acc0, acc1, gt_out ? kFeProgram : kFeProgramVerify, slot,
+                                         LdsF12{park, wave_first_thread()});
       const GlobF12W acc = which ? acc1 : acc0;
-      if (!is_one12(acc)) c = CODE_PAIRING;
+      if (!(gt_out ? is_one12(acc) : is_conj12(acc, slot(SL_T4)))) c = CODE_PAIRING;
       if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
 #pragma unroll 1
         for (int k = 0; k < 6; k++) {

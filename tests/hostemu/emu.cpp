@@ -271,7 +271,13 @@ int emu_verify(const uint8_t* sig, const uint8_t* msg, uint32_t mlen, const uint
     const fp* e = &g.c0.c0.c0;
     for (int i = 0; i < 12; i++) raw_to_be48(from_mont(e[i]), gt_out + 48 * i);
   }
-  return is_one(g) ? 0 : 5;
+  const int code = is_one(g) ? 0 : 5;
+  // k_final's verdict-only program (no last multiply, conj comparison) must agree
+  static const uint8_t progv[][2] = {CESS_FE_PROGRAM_VERIFY};
+  const int w2 = final_exp_staged(ArrF12{&acc}, ArrF12{&acc1}, progv, [](int sl) { return ArrF12{&slots[sl]}; },
+                                  ArrF12{&park});
+  const int code_v = is_conj12(ArrF12{w2 ? &acc1 : &acc}, ArrF12{&slots[SL_T4]}) ? 0 : 5;
+  return code_v == code ? code : 99;
 }
 
 // value-based Miller loop + final exponentiation (pairing.hpp) for the same record

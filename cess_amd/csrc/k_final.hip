@@ -39,19 +39,25 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
       auto slot = [&](int s) {
         return GlobF12W{(s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride) + w0, stride};
       };
-      const int which = final_exp_staged(acc0, acc1, gt_out ? kFeProgram : kFeProgramVerify, slot,
-                                         LdsF12{park, wave_first_thread()});
-      const GlobF12W acc = which ? acc1 : acc0;
-      if (!(gt_out ? is_one12(acc) : is_conj12(acc, slot(SL_T4)))) c = CODE_PAIRING;
-      if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
+      // f = 1 (an (O, O) record: both Miller terms skipped) has f^e = 1: the
+      // verdict is OK without the exponentiation, and the lane does not take
+      // the Karabina fallback (z2 = z3 = 0 redoes every chain in Granger-Scott
+      // form, for its whole wave).  (Gt bytes requested: the full program.)
+      if (gt_out || !is_one12(slot(SL_F))) {
+        const int which = final_exp_staged(acc0, acc1, gt_out ? kFeProgram : kFeProgramVerify, slot,
+                                           LdsF12{park, wave_first_thread()});
+        const GlobF12W acc = which ? acc1 : acc0;
+        if (!(gt_out ? is_one12(acc) : is_conj12(acc, slot(SL_T4)))) c = CODE_PAIRING;
+        if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
 #pragma unroll 1
-        for (int k = 0; k < 6; k++) {
-          fp2 e = acc.ld(k);
-          uint8_t b[48];
-          raw_to_be48(from_mont(e.c0), b);
-          for (int t = 0; t < 48; t++) gt_out[576 * (uint64_t)i + 96 * k + t] = b[t];
-          raw_to_be48(from_mont(e.c1), b);
-          for (int t = 0; t < 48; t++) gt_out[576 * (uint64_t)i + 96 * k + 48 + t] = b[t];
+          for (int k = 0; k < 6; k++) {
+            fp2 e = acc.ld(k);
+            uint8_t b[48];
+            raw_to_be48(from_mont(e.c0), b);
+            for (int t = 0; t < 48; t++) gt_out[576 * (uint64_t)i + 96 * k + t] = b[t];
+            raw_to_be48(from_mont(e.c1), b);
+            for (int t = 0; t < 48; t++) gt_out[576 * (uint64_t)i + 96 * k + 48 + t] = b[t];
+          }
         }
       }
       code[i] = c;

@@ -38,11 +38,21 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   // (156.6 vs 156.3 ms, profiles/round3_n_sweep.txt).  Row addresses formed
   // as a uniform base + a 32-bit lane byte offset (global_load voffset,
   // s[base]) measured slower (159.2 ms).
+#if defined(CESS_PROBE_PTREG)   // timing probe
+  const g1a p0{ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), false};
+  const g1a p1{ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), false};
+  auto pt = [&](int pair) { return pair ? p1 : p0; };
+#else
   auto pt = [&](int pair) {
     const uint32_t* b = pair ? h_aff : sig_aff;
     return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
   };
+#endif
+#if defined(CESS_PROBE_NOLOAD)   // timing probe: pair 1 reads the uniform table (wrong verdicts)
+  auto src = [&](int pair, int k) { return ld_coeff_uniform(neg_g2, k + pair * 0); };
+#else
   auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, cstride, cj, k) : ld_coeff_uniform(neg_g2, k); };
+#endif
   // cnorm (keyed batches): the key's lines were normalised to c2 = 1
   // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0.
   // (Per-signature rows are not normalised: k_norm_keys over every record

@@ -248,6 +248,8 @@ static bool offsets_ok(size_t n, const uint64_t* o) {
     if (o[i + 1] < o[i]) return false;
   return true;
 }
+// a data buffer may be null only if its records are all empty
+static bool data_ok(size_t n, const uint8_t* d, const uint64_t* o) { return d || o[n] == o[0]; }
 
 extern "C" int cess_bls_cache_insert_var(cess_bls_cache* cache, size_t n, const uint8_t* sig_data,
                                          const uint64_t* sig_offsets, const uint8_t* pk_data,
@@ -256,7 +258,8 @@ extern "C" int cess_bls_cache_insert_var(cess_bls_cache* cache, size_t n, const 
   if (!cache) return CESS_BLS_E_INVALID_ARG;
   if (n == 0) return CESS_BLS_OK;
   if (!sig_offsets || !pk_offsets || !msg_offsets || !codes || !offsets_ok(n, sig_offsets) ||
-      !offsets_ok(n, pk_offsets) || !offsets_ok(n, msg_offsets))
+      !offsets_ok(n, pk_offsets) || !offsets_ok(n, msg_offsets) || !data_ok(n, sig_data, sig_offsets) ||
+      !data_ok(n, pk_data, pk_offsets) || !data_ok(n, msgs, msg_offsets))
     return CESS_BLS_E_INVALID_ARG;
   for (size_t i = 0; i < n; i++)
     if (codes[i] > CESS_BLS_CODE_PAIRING_FAIL) return CESS_BLS_E_INVALID_ARG;   // verdicts only
@@ -278,7 +281,8 @@ extern "C" int cess_bls_cache_verify_var(cess_bls_cache* cache, cess_bls_ctx* ct
   if (stats3) stats3[0] = stats3[1] = stats3[2] = 0;
   if (n == 0) return CESS_BLS_OK;
   if (!sig_offsets || !pk_offsets || !msg_offsets || !codes_out || !offsets_ok(n, sig_offsets) ||
-      !offsets_ok(n, pk_offsets) || !offsets_ok(n, msg_offsets))
+      !offsets_ok(n, pk_offsets) || !offsets_ok(n, msg_offsets) || !data_ok(n, sig_data, sig_offsets) ||
+      !data_ok(n, pk_data, pk_offsets) || !data_ok(n, msgs, msg_offsets))
     return CESS_BLS_E_INVALID_ARG;
   std::vector<Digest> dg(n);
   for (size_t i = 0; i < n; i++)

@@ -68,6 +68,28 @@ def test_cache_hits_dedup_and_fifo_eviction():
     assert len(c) == 0
 
 
+def test_cache_rejects_null_data_with_nonempty_records():
+    """A null record buffer is accepted only when all its records are empty
+    (the C ABI reads nothing then); otherwise INVALID_ARG, not a crash."""
+    import ctypes
+    lib = bls.load_library()
+    c = bls.VerdictCache(4)
+    u64 = ctypes.c_uint64 * 2
+    sig = (ctypes.c_uint8 * 48)()
+    pk = (ctypes.c_uint8 * 96)()
+    codes = (ctypes.c_uint8 * 1)(0)
+    for so, sd, po, pd, mo in ((u64(0, 48), None, u64(0, 96), pk, u64(0, 0)),      # sigs null, 48 bytes claimed
+                               (u64(0, 48), sig, u64(0, 96), None, u64(0, 0)),      # keys null
+                               (u64(0, 48), sig, u64(0, 96), pk, u64(0, 32))):      # msgs null, 32 bytes claimed
+        st = lib.cess_bls_cache_verify_var(c._h, None, 1, sd, so, pd, po, None, mo, codes, None)
+        assert st == bls.E_INVALID_ARG
+        st = lib.cess_bls_cache_insert_var(c._h, 1, sd, so, pd, po, None, mo, codes)
+        assert st == bls.E_INVALID_ARG
+    # empty messages with a null message buffer are fine (no device: unavailable)
+    st = lib.cess_bls_cache_verify_var(c._h, None, 1, sig, u64(0, 48), pk, u64(0, 96), None, u64(0, 0), codes, None)
+    assert st == bls.E_NO_DEVICE and codes[0] == bls.CODE_UNAVAILABLE
+
+
 def _golden_records(vectors):
     cases = vectors["cases"] + vectors["length_cases"]
     return [(bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])) for c in cases], \

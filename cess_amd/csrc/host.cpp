@@ -435,6 +435,9 @@ int cess_host::verify_var_host(cess_bls_ctx* c, size_t n, const uint8_t* sig_dat
                                const uint64_t* msg_offsets, uint8_t* codes_out, uint64_t* bitmap_out) {
   if (!sig_offsets || !pk_offsets || !msg_offsets) return CESS_BLS_E_INVALID_ARG;
   if (n == 0) return CESS_BLS_OK;
+  // a null record buffer only with all its records empty
+  if ((!sig_data && sig_offsets[n] != sig_offsets[0]) || (!pk_data && pk_offsets[n] != pk_offsets[0]))
+    return CESS_BLS_E_INVALID_ARG;
   std::vector<uint8_t> sigs(n * 48, 0), pks(n * 96, 0), pre(n, 0);
   for (size_t i = 0; i < n; i++) {
     if (sig_offsets[i + 1] < sig_offsets[i] || pk_offsets[i + 1] < pk_offsets[i]) return CESS_BLS_E_INVALID_ARG;

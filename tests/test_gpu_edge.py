@@ -47,6 +47,24 @@ def test_empty_batch(ctx):
     assert codes == b"" and words == []
 
 
+def test_var_batch_null_buffers(ctx):
+    """cess_bls_verify_batch_var: a null signature / key buffer is accepted only
+    when every record of it is empty (all WrongLength); otherwise INVALID_ARG."""
+    import ctypes
+    from cess_amd import bls
+    lib = ctx._lib
+    u64 = ctypes.c_uint64 * 2
+    codes = (ctypes.c_uint8 * 1)()
+    pk = (ctypes.c_uint8 * 96)()
+    sig = (ctypes.c_uint8 * 48)()
+    st = lib.cess_bls_verify_batch_var(ctx._h, 1, None, u64(0, 48), pk, u64(0, 96), None, u64(0, 0), codes, None)
+    assert st == bls.E_INVALID_ARG
+    st = lib.cess_bls_verify_batch_var(ctx._h, 1, sig, u64(0, 48), None, u64(0, 96), None, u64(0, 0), codes, None)
+    assert st == bls.E_INVALID_ARG
+    st = lib.cess_bls_verify_batch_var(ctx._h, 1, None, u64(0, 0), pk, u64(0, 96), None, u64(0, 0), codes, None)
+    assert st == 0 and codes[0] == 1             # empty signature: SIG_LEN, nothing read
+
+
 def _hip():
     """The HIP runtime libcess_bls.so itself links (/opt/rocm), via ctypes, so
     device buffers come from the same runtime instance as the kernels (torch

@@ -22,6 +22,8 @@ __global__ void k_rsa_classify(uint64_t, const uint32_t*, uint32_t, const RsaKey
 RSA_KERNEL_DECL(k_rsa_verify_1024)
 RSA_KERNEL_DECL(k_rsa_verify_2048)
 RSA_KERNEL_DECL(k_rsa_verify_2048u)
+__global__ void k_rsa_verify_big(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const RsaKeyDev*,
+                                 const uint8_t*, const uint64_t*, const uint8_t*, const uint64_t*, uint8_t*);
 __global__ void k_rsa_count(uint64_t, const uint32_t*, uint32_t, const RsaKeyDev*, const uint8_t*, const uint64_t*,
                             const uint64_t*, uint8_t*, uint32_t*);
 __global__ void k_rsa_scan(uint32_t, const uint32_t*, uint32_t*, uint32_t*);
@@ -117,10 +119,15 @@ bool parse_spki(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t&
   return parse_pkcs1(bits.v + 1, bits.len - 1, mod, e);
 }
 
-int size_class_limbs(size_t bits) {
+// limbs of the key's size class: the expanded 1024 / 2048-bit classes, or
+// (2049..4096 bits, k_rsa_verify_big) the least L with 28 L >= 8 k + 2, so that
+// every bit of a k-byte signature has a limb (the s < n check sees all of it)
+// and R = 2^(28 L) >= 4n
+int size_class_limbs(size_t bits, size_t k_bytes) {
   if (bits + 2 <= 28 * RSA_L1024) return RSA_L1024;
   if (bits + 2 <= 28 * RSA_L2048) return RSA_L2048;
-  return 0;   // 2049..4096-bit moduli: parsed by the reference, not supported here
+  const int L = (int)((8 * k_bytes + 2 + 27) / 28);
+  return L <= RSA_LMAX ? L : 0;
 }
 
 // big-endian bytes -> L 28-bit limbs (little-endian)
@@ -184,6 +191,7 @@ void key_row(const std::vector<uint8_t>& mod, uint64_t e, int L, RsaKeyDev& k) {
 struct RsaTable {
   DevBuf keys, ok;
   uint32_t n = 0;
+  bool big = false;   // a key of the loop-form class (2049-4096 bits)
 };
 struct RsaState {
   RsaTable user, single;
@@ -203,6 +211,7 @@ static int load_table(cess_bls_ctx* c, RsaTable& T, size_t k, const uint8_t* der
                       int* status_out) {
   std::vector<RsaKeyDev> rows(std::max<size_t>(k, 1));
   std::vector<uint8_t> ok(std::max<size_t>(k, 1), 0);
+  bool big = false;
   for (size_t j = 0; j < k; j++) {
     std::vector<uint8_t> mod;
     uint64_t e = 0;
@@ -218,12 +227,13 @@ static int load_table(cess_bls_ctx* c, RsaTable& T, size_t k, const uint8_t* der
     if (st == CESS_BLS_OK) {
       size_t bits = 8 * mod.size();
       for (uint8_t v = mod[0]; !(v & 0x80); v <<= 1) bits--;
-      L = size_class_limbs(bits);
+      L = size_class_limbs(bits, mod.size());
       if (!L) st = CESS_RSA_E_UNSUPPORTED;
     }
     if (st == CESS_BLS_OK) {
       key_row(mod, e, L, rows[j]);
       ok[j] = 1;
+      big = big || L > RSA_L2048;
     } else {
       memset(&rows[j], 0, sizeof(RsaKeyDev));
     }
@@ -234,6 +244,7 @@ static int load_table(cess_bls_ctx* c, RsaTable& T, size_t k, const uint8_t* der
   HIPCHK(hipMemcpy(T.keys.p, rows.data(), rows.size() * sizeof(RsaKeyDev), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(T.ok.p, ok.data(), ok.size(), hipMemcpyHostToDevice));
   T.n = (uint32_t)k;
+  T.big = big;
   return CESS_BLS_OK;
 }
 
@@ -249,9 +260,9 @@ static int rsa_run(cess_bls_ctx* c, RsaTable& T, hipStream_t s, uint64_t n, cons
   // Few keys with many records each (the TEE-key workload): key-sorted,
   // wave-padded lists, so each wave of the 2048-bit kernel has one key and its
   // modulus is a scalar operand (k_rsa_2048u).  Otherwise unsorted lists.
-  if (T.n > 0 && T.n <= kRsaUniformMaxKeys && n >= kRsaUniformMinPerKey * (uint64_t)T.n) {
+  if (!T.big && T.n > 0 && T.n <= kRsaUniformMaxKeys && n >= kRsaUniformMinPerKey * (uint64_t)T.n) {
     const uint64_t nk = T.n, cap = n + 64 * nk;   // each (class, key) segment pads < 64 entries
-    if (S.lists.ensure(2 * cap * 4) | S.counts.ensure((6 * nk + 2) * 4) | S.base.ensure(cap * RSA_LMAX * 4))
+    if (S.lists.ensure(2 * cap * 4) | S.counts.ensure((6 * nk + 2) * 4) | S.base.ensure(cap * RSA_L2048 * 4))
       return CESS_BLS_E_OOM;
     uint32_t* cnt = S.counts.as<uint32_t>();
     uint32_t *cur = cnt + 2 * nk, *segbase = cnt + 4 * nk, *totals = cnt + 6 * nk;
@@ -281,7 +292,7 @@ static int rsa_run(cess_bls_ctx* c, RsaTable& T, hipStream_t s, uint64_t n, cons
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;
   }
-  if (S.lists.ensure(2 * n * 4) | S.counts.ensure(16) | S.base.ensure(n * RSA_LMAX * 4)) return CESS_BLS_E_OOM;
+  if (S.lists.ensure(3 * n * 4) | S.counts.ensure(16) | S.base.ensure(n * RSA_L2048 * 4)) return CESS_BLS_E_OOM;
   HIPCHK(hipMemsetAsync(S.counts.p, 0, 16, s));
   // per-launch HIP events on s (CESS_BLS_F_PROFILE): bench.py's roofline
   // takes the verification kernel's duration from them
@@ -303,6 +314,9 @@ static int rsa_run(cess_bls_ctx* c, RsaTable& T, hipStream_t s, uint64_t n, cons
                      d_sigs, d_soffs, d_msgs, d_moffs, B, d_codes);
   hipLaunchKernelGGL(k_rsa_verify_1024, dim3(grid_for(n)), dim3(kBlock), 0, s, (uint32_t)n, cnt, L, d_idx, K, d_sigs,
                      d_soffs, d_msgs, d_moffs, B, d_codes);
+  if (T.big)   // 2049-4096-bit moduli (list 2)
+    hipLaunchKernelGGL(k_rsa_verify_big, dim3(grid_for(n)), dim3(kBlock), 0, s, (uint32_t)n, cnt + 2, L + 2 * n, d_idx,
+                       K, d_sigs, d_soffs, d_msgs, d_moffs, d_codes);
   r = prof_end(c, s, ST_RSA_VERIFY, a);
   if (r) return r;
   HIPCHK(hipGetLastError());

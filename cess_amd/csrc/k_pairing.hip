@@ -31,15 +31,13 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   uint8_t fl = inf[i];
   __shared__ uint4 F[36][256];
   LdsF12 f{F, wave_first_thread()};
-  // the two G1 points live in registers for the whole loop (48 dwords): the
-  // lane-fresh LDS addressing left k_miller without scratch, so holding them
-  // costs no spill, and the loop stops re-reading 13 KB per signature of
-  // points from L2 every line (time unchanged: 156.6 vs 156.3 ms per 1 M,
-  // profiles/round3_n_sweep.txt; counted traffic round3_z).  (With the
-  // round-2 register allocation they spilled: 163 -> 171 ms.)
-  const g1a p0{ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), false};
-  const g1a p1{ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), false};
-  auto pt = [&](int pair) { return pair ? p1 : p0; };
+  // the G1 points are re-read from L2 for every line: held in 48 registers
+  // across the loop they cost 27 spilled VGPRs (112 B/lane of scratch) and
+  // +0.4 ms (profiles/round3_z_sweep.txt; round 2: 163 -> 171 ms)
+  auto pt = [&](int pair) {
+    const uint32_t* b = pair ? h_aff : sig_aff;
+    return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
+  };
   auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, cstride, cj, k) : ld_coeff_uniform(neg_g2, k); };
   // cnorm (keyed batches): the key's lines were normalised to c2 = 1
   // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0.

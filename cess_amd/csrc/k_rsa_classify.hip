@@ -1,14 +1,16 @@
 // RSA batch front end (see k_rsa.hpp): per record, the length checks of
 // rsa 0.8.2's pkcs1v15 verify (sig.len() == k, k >= msg.len() + 11) and the
 // key lookup; records that pass are appended to their size class's list
-// (1024 / 2048-bit moduli), the others get their final code here.
+// (1024 / 2048-bit moduli, and 2049-4096 for the loop-form kernel), the
+// others get their final code here.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
 #include "rsa.hpp"
 
 // the length checks and key lookup of one record: its size class (0: 1024,
-// 1: 2048-bit modulus) or -1 with its final code written (codes may be null)
+// 1: 2048-bit modulus, 2: larger) or -1 with its final code written (codes may
+// be null)
 __device__ __forceinline__ int rsa_class(uint64_t r, uint64_t n, const uint32_t* __restrict__ key_idx, uint32_t nkeys,
                                          const RsaKeyDev* __restrict__ keys, const uint8_t* __restrict__ key_ok,
                                          const uint64_t* __restrict__ sig_offs, const uint64_t* __restrict__ msg_offs,
@@ -29,7 +31,7 @@ __device__ __forceinline__ int rsa_class(uint64_t r, uint64_t n, const uint32_t*
     if (codes) codes[r] = RSA_MSG_LEN;
     return -1;
   }
-  return K.limbs == RSA_L1024 ? 0 : 1;
+  return K.limbs == RSA_L1024 ? 0 : K.limbs == RSA_L2048 ? 1 : 2;
 }
 
 // wave-aggregated atomicAdd(&ctr[slot], 1) for the lanes with slot >= 0; returns
@@ -53,6 +55,7 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* __restrict__ ctr, int6
 // Key-uniform path (few keys, many records each): records of each (class,
 // key) are placed in a segment of the class list whose start is a multiple of
 // 64, so every wave of the verification kernel sees one key (k_rsa_2048u).
+// Only taken for tables without keys of the loop-form class (classes 0, 1).
 // count -> scan -> scatter; slots are cls * nkeys + key.
 __global__ __launch_bounds__(256) void k_rsa_count(uint64_t n, const uint32_t* __restrict__ key_idx, uint32_t nkeys,
                                                    const RsaKeyDev* __restrict__ keys,
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(256) void k_rsa_classify(uint64_t n, const uint32_t
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1;
 #pragma unroll
-  for (int c = 0; c < 2; c++) {
+  for (int c = 0; c < 3; c++) {
     const uint64_t mask = __ballot(cls == c);
     if (!mask) continue;
     const int leader = __ffsll((unsigned long long)mask) - 1;

@@ -3,12 +3,16 @@
 #include <stdint.h>
 
 // 28-bit limbs per size class: R = 2^(28 L) >= 4n for moduli of up to
-// 1024 / 2048 bits (28 L >= bits + 2).  (A 3072-bit class, L = 110, was built
-// and took 28 minutes to compile as a fully expanded product scan; Podr2Key is
-// 2048-bit, so larger keys report CESS_RSA_E_UNSUPPORTED.)
+// 1024 / 2048 bits (28 L >= bits + 2), expanded at compile time
+// (k_rsa_verify_1024 / _2048 / _2048u).  Moduli of 2049-4096 bits (the rest of
+// what rsa 0.8's from_public_key_der accepts) take the loop-form kernel
+// k_rsa_verify_big with L = ceil((bits + 2) / 28) <= RSA_L4096 limbs chosen per
+// key at run time (a fully expanded 3072-bit class, L = 110, took 28 minutes
+// to compile).
 #define RSA_L1024 37
 #define RSA_L2048 74
-#define RSA_LMAX RSA_L2048
+#define RSA_L4096 147
+#define RSA_LMAX RSA_L4096
 
 // an inactive entry of a wave-padded record list (k_rsa_scatter)
 #define RSA_PAD 0xffffffffu

@@ -11,10 +11,11 @@
  *
  * Per-signature codes: 0 OK, 1 SIG_LEN (len != k), 2 SIG_RANGE (s >= n),
  * 3 MSG_LEN (k < len(msg) + 11), 4 MISMATCH, 5 KEY (no such key / the key did
- * not load).  Codes 1..5 are the reference's `false`.  Moduli of up to 2048
- * bits are verified on the GPU (1024/2048-bit size classes; Podr2Key is a
- * 2048-bit key).  Keys the reference accepts but the GPU cannot verify --
- * 2049..4096-bit moduli, even moduli, n < 3, SPKI AlgorithmIdentifier
+ * not load).  Codes 1..5 are the reference's `false`.  Every modulus size
+ * the crate accepts (up to 4096 bits) is verified on the GPU: 1024/2048-bit
+ * size classes expanded at compile time (Podr2Key is a 2048-bit key) and a
+ * loop-form kernel for 2049..4096 bits.  Keys the reference accepts but the
+ * GPU cannot verify -- even moduli, n < 3, SPKI AlgorithmIdentifier
  * parameters other than NULL -- report CESS_RSA_E_UNSUPPORTED, never
  * CESS_BLS_E_BAD_KEY: the verdict path for them is the caller's (the node
  * hook answers "unavailable" and the runtime's unchanged

@@ -1,6 +1,7 @@
 """Generate tests/golden/rsa_vectors.json from the RSA oracle (oracle/rsa_oracle.py).
 
-Deterministic (seeded) keys of 1024 / 2048 / 3072 bits, e = 65537 and e = 3,
+Deterministic (seeded) keys of 1024 / 2048 / 2071 / 3001 / 3072 / 4096 bits,
+e = 65537 and e = 3,
 each as SPKI DER (what cp_enclave_verify::verify_rsa parses) and PKCS#1 DER
 (Podr2Key = [u8; 270], primitives/common/src/lib.rs:54), with valid and
 invalid raw PKCS#1 v1.5 signatures (Pkcs1v15Sign::new_raw()) -- including the
@@ -97,6 +98,36 @@ def main():
     for _ in range(256):
         m = bytes(rng.randrange(256) for _ in range(32))
         pool.append({"msg": m.hex(), "sig": o.sign_raw(n0, d0, m).hex()})
+    # moduli of the loop-form GPU class (2049-4096 bits, k_rsa_verify_big):
+    # 4096 bits (the crate's maximum), 2071 bits (the smallest size above the
+    # 2048-bit class, 75 limbs) and 3001 bits with e = 3, from their own seed
+    # so the vectors above stay as they were
+    rng2 = random.Random(0x52534132)
+    for bits, e in ((4096, 65537), (2071, 65537), (3001, 3)):
+        n, e, d = o.gen_key(bits, e, rng2)
+        keys.append({"n": n, "e": e, "d": d})
+        out_keys.append({"bits": n.bit_length(), "e": e, "spki": o.encode_spki(n, e).hex(),
+                         "pkcs1": o.encode_pkcs1(n, e).hex()})
+        ki = len(keys) - 1
+        kb = (n.bit_length() + 7) // 8
+        hw = b"hello world!"
+        s = o.sign_raw(n, d, hw)
+        add(f"k{ki}_hello_world", ki, hw, s)
+        for j in range(2):
+            m = bytes(rng2.randrange(256) for _ in range(32))
+            add(f"k{ki}_valid32_{j}", ki, m, o.sign_raw(n, d, m))
+        mx = bytes(rng2.randrange(256) for _ in range(kb - 11))
+        add(f"k{ki}_max_msg", ki, mx, o.sign_raw(n, d, mx))
+        add(f"k{ki}_empty_msg", ki, b"", o.sign_raw(n, d, b""))
+        add(f"k{ki}_wrong_msg", ki, b"hello world?", s)
+        add(f"k{ki}_flipped_sig", ki, hw, s[:-1] + bytes([s[-1] ^ 1]))
+        add(f"k{ki}_short_sig", ki, hw, s[1:])
+        add(f"k{ki}_sig_eq_n", ki, hw, n.to_bytes(kb, "big"))
+        add(f"k{ki}_sig_max", ki, hw, b"\xff" * kb)
+        add(f"k{ki}_sig_one", ki, b"", (1).to_bytes(kb, "big"))
+        add(f"k{ki}_msg_too_long", ki, bytes(kb - 10), s)
+        em = b"\x00\x02" + b"\xff" * (kb - len(hw) - 3) + b"\x00" + hw
+        add(f"k{ki}_bt02", ki, hw, pow(int.from_bytes(em, "big"), d, n).to_bytes(kb, "big"))
     doc = {"generator": "tests/golden/gen_rsa.py (oracle/rsa_oracle.py)",
            "codes": {"0": "OK", "1": "SIG_LEN", "2": "SIG_RANGE", "3": "MSG_LEN", "4": "MISMATCH"},
            "keys": out_keys, "cases": cases, "bad_keys": bad_keys,

@@ -83,19 +83,20 @@ def test_gpu_fixture_codes(rv):
     c = _gpu_ctx()
     try:
         st = c.rsa_keys_load([bytes.fromhex(k["spki"]) for k in rv["keys"]])
-        # 1024 / 2048-bit keys load; the 3072-bit key is beyond the GPU size classes
-        assert st == [0 if k["bits"] <= 2048 else bls.RSA_E_UNSUPPORTED for k in rv["keys"]]
+        # every size the crate accepts loads: 1024 / 2048-bit classes and the
+        # loop-form class (2071, 3001, 3072, 4096 bits)
+        assert st == [0] * len(rv["keys"])
         cases = rv["cases"]
         codes = c.rsa_verify_batch([x["key"] for x in cases], [bytes.fromhex(x["msg"]) for x in cases],
                                    [bytes.fromhex(x["sig"]) for x in cases])
         for x, got in zip(cases, codes):
-            bits = rv["keys"][x["key"]]["bits"]
-            assert got == (x["code"] if bits <= 2048 else 5), x["name"]
+            assert got == x["code"], x["name"]
+        assert any(k["bits"] > 2048 for k in rv["keys"]) and any(k["bits"] == 4096 for k in rv["keys"])
         # the PKCS#1 (Podr2Key) encoding gives the same table
-        assert c.rsa_keys_load([bytes.fromhex(k["pkcs1"]) for k in rv["keys"]], bls.RSA_KEY_PKCS1)[:3] == [0, 0, 0]
-        sel = [x for x in cases if rv["keys"][x["key"]]["bits"] <= 2048]
-        assert c.rsa_verify_batch([x["key"] for x in sel], [bytes.fromhex(x["msg"]) for x in sel],
-                                  [bytes.fromhex(x["sig"]) for x in sel]) == bytes(x["code"] for x in sel)
+        assert c.rsa_keys_load([bytes.fromhex(k["pkcs1"]) for k in rv["keys"]], bls.RSA_KEY_PKCS1) == \
+            [0] * len(rv["keys"])
+        assert c.rsa_verify_batch([x["key"] for x in cases], [bytes.fromhex(x["msg"]) for x in cases],
+                                  [bytes.fromhex(x["sig"]) for x in cases]) == bytes(x["code"] for x in cases)
         # out-of-range key index -> KEY
         assert c.rsa_verify_batch([9], [b"x"], [bytes(256)]) == bytes([5])
     finally:
@@ -110,12 +111,7 @@ def test_gpu_verify_rsa_dropin(rv):
         for x in rv["cases"]:
             k = rv["keys"][x["key"]]
             der, msg, sig = bytes.fromhex(k["spki"]), bytes.fromhex(x["msg"]), bytes.fromhex(x["sig"])
-            if k["bits"] > 2048:
-                with pytest.raises(bls.BlsInfraError) as ei:
-                    c.verify_rsa(der, msg, sig)
-                assert ei.value.status == bls.RSA_E_UNSUPPORTED
-                continue
-            assert c.verify_rsa(der, msg, sig) == (x["code"] == 0), x["name"]
+            assert c.verify_rsa(der, msg, sig) == (x["code"] == 0), x["name"]   # every size: a verdict
         for b in rv["bad_keys"]:
             with pytest.raises(bls.BlsInfraError) as ei:
                 c.verify_rsa(bytes.fromhex(b["der"]), b"hello world!", bytes(256))
@@ -130,6 +126,33 @@ def test_gpu_verify_rsa_dropin(rv):
         assert st == [bls.RSA_E_UNSUPPORTED] * len(rv["unsupported_keys"])
     finally:
         c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_sizes_device_batch(rv):
+    """Records of all size classes interleaved in one batch (the classify
+    kernel's three lists): codes equal the oracle's, including bit flips and
+    wrong lengths under the 2049-4096-bit keys."""
+    from cess_amd import bls
+    rng = random.Random(12)
+    parsed = [o.parse_spki(bytes.fromhex(k["spki"])) for k in rv["keys"]]
+    recs = []
+    for _ in range(600):
+        x = rng.choice(rv["cases"])
+        msg, sig = bytes.fromhex(x["msg"]), bytes.fromhex(x["sig"])
+        if rng.random() < 0.3 and sig:
+            sig = sig[:-1] + bytes([sig[-1] ^ rng.randrange(1, 256)])
+        n, e = parsed[x["key"]]
+        recs.append((x["key"], msg, sig, o.verify_code(n, e, msg, sig)))
+    c = _gpu_ctx()
+    try:
+        assert c.rsa_keys_load([bytes.fromhex(k["spki"]) for k in rv["keys"]]) == [0] * len(rv["keys"])
+        got = c.rsa_verify_batch([r[0] for r in recs], [r[1] for r in recs], [r[2] for r in recs])
+    finally:
+        c.close()
+    assert list(got) == [r[3] for r in recs]
+    big = [g for r, g in zip(recs, got) if rv["keys"][r[0]]["bits"] > 2048]
+    assert {0, 4} <= set(big)
 
 
 @pytest.mark.gpu

@@ -33,7 +33,7 @@ pub enum Error {
     /// shared-memory communicator: a peer timed out / the transport failed
     Comm,
     /// RSA: the key parses (the reference accepts it) but the GPU cannot
-    /// verify it (> 2048-bit, even modulus, non-NULL SPKI parameters); the
+    /// verify it (even modulus, n < 3, non-NULL SPKI parameters); the
     /// caller's own path decides (include/cess_rsa.h)
     Unsupported,
     Other(i32),
@@ -571,7 +571,7 @@ pub fn verify_bls(key: &[u8], msg: &[u8], sig: &[u8]) -> Result<(), ()> {
 /// not parse as SubjectPublicKeyInfo DER.
 ///
 /// DIVERGENCE (documented): a key the reference parses but the GPU
-/// cannot verify (> 2048-bit modulus, even modulus, non-NULL SPKI parameters;
+/// cannot verify (even modulus, n < 3, non-NULL SPKI parameters;
 /// `Error::Unsupported`) also panics here, where the reference returns a
 /// verdict.  Callers that must not panic on such keys use `try_verify_rsa` and
 /// route `Err(Error::Unsupported)` to their own path (the node hook answers

@@ -120,14 +120,15 @@ bool parse_spki(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t&
 }
 
 // limbs of the key's size class: the expanded 1024 / 2048-bit classes, or
-// (2049..4096 bits, k_rsa_verify_big) the least L with 28 L >= 8 k + 2, so that
-// every bit of a k-byte signature has a limb (the s < n check sees all of it)
-// and R = 2^(28 L) >= 4n
+// (2049..4096 bits, k_rsa_verify_big) the least multiple of RSA_BIG_ROWS with
+// 28 L >= 8 k + 2, so that every bit of a k-byte signature has a limb (the
+// s < n check sees all of it) and R = 2^(28 L) >= 4n
 int size_class_limbs(size_t bits, size_t k_bytes) {
   if (bits + 2 <= 28 * RSA_L1024) return RSA_L1024;
   if (bits + 2 <= 28 * RSA_L2048) return RSA_L2048;
-  const int L = (int)((8 * k_bytes + 2 + 27) / 28);
-  return L <= RSA_LMAX ? L : 0;
+  const int L0 = (int)((8 * k_bytes + 2 + 27) / 28);
+  const int L = (L0 + RSA_BIG_ROWS - 1) / RSA_BIG_ROWS * RSA_BIG_ROWS;
+  return L0 <= RSA_L4096 ? L : 0;
 }
 
 // big-endian bytes -> L 28-bit limbs (little-endian)

@@ -2,9 +2,10 @@
 // size class).  Same verification as k_rsa.hpp (reference:
 // primitives/enclave-verify/src/lib.rs:221-228, rsa 0.8.2
 // RsaPublicKey::verify(Pkcs1v15Sign::new_raw(), msg, sig)) with the limb count
-// L = K.limbs a run-time value: Montgomery products in the finely integrated
-// operand-scanning form (FIOS: one pass per digit of a, 28-bit digits, 64-bit
-// column values, never more than 2^58) over per-lane arrays in private memory.
+// L = K.limbs a run-time value: Montgomery products in finely integrated
+// operand-scanning form (FIOS, 28-bit digits, 64-bit column values never above
+// 2^58), RSA_BIG_ROWS rows per pass as a systolic chain (rsa_mont.hpp), over
+// per-lane arrays in private memory.
 // Keys of these sizes are rare (Podr2Key is 2048-bit,
 // primitives/common/src/lib.rs:54): the kernel exists so that every key the
 // reference verifies gets a GPU verdict, not for throughput.
@@ -12,36 +13,9 @@
 
 #include "kernels.hpp"
 #include "rsa.hpp"
+#include "rsa_mont.hpp"
 
-namespace {
-
-constexpr uint32_t M28 = 0x0fffffffu;
-
-// out = a b R^-1 mod n, in [0, 2n) for a, b < 2n (4n <= R = 2^(28 L));
-// out must not alias a or b
-__device__ void mont_rt(const uint32_t* a, const uint32_t* b, const uint32_t* __restrict__ n, uint32_t ninv, int L,
-                        uint32_t* out) {
-  uint32_t t[RSA_LMAX + 1];
-  for (int j = 0; j <= L; j++) t[j] = 0;
-  for (int i = 0; i < L; i++) {
-    const uint64_t ai = a[i];
-    uint64_t u = t[0] + ai * b[0];
-    const uint64_t m = ((uint32_t)u * ninv) & M28;
-    u += m * n[0];
-    uint64_t c = u >> 28;   // the low 28 bits are zero
-    for (int j = 1; j < L; j++) {
-      u = t[j] + ai * b[j] + m * n[j] + c;   // < 2^28 + 2^57 + 2^37: no overflow
-      t[j - 1] = (uint32_t)u & M28;
-      c = u >> 28;
-    }
-    u = t[L] + c;
-    t[L - 1] = (uint32_t)u & M28;
-    t[L] = (uint32_t)(u >> 28);
-  }
-  for (int j = 0; j < L; j++) out[j] = t[j];   // t[L] = 0: the result is < 2n < R
-}
-
-}  // namespace
+using namespace rsa_big;
 
 // rec: this class's record list (its length at *cnt), key_idx / keys / the
 // record buffers as k_rsa_verify_2048.  One lane per record.
@@ -62,7 +36,7 @@ __global__ __launch_bounds__(256) void k_rsa_verify_big(uint32_t n_max, const ui
   const int L = (int)K.limbs, kb = (int)K.k_bytes;
   if (L <= 0 || L > RSA_LMAX) return;   // the host never builds such a row
   const uint32_t* n = K.n28;
-  uint32_t x[RSA_LMAX], base[RSA_LMAX], y[RSA_LMAX];
+  uint32_t x[RSA_LMAX + 1], base[RSA_LMAX + 1], y[RSA_LMAX + 1];
   // s = OS2IP(sig) -> 28-bit limbs (bit k of s = bit k % 8 of byte kb - 1 - k / 8)
   const uint8_t* sg = sigs + sig_offs[r];
   for (int q = 0; q < L; q++) x[q] = 0;

@@ -6,13 +6,17 @@
 // 1024 / 2048 bits (28 L >= bits + 2), expanded at compile time
 // (k_rsa_verify_1024 / _2048 / _2048u).  Moduli of 2049-4096 bits (the rest of
 // what rsa 0.8's from_public_key_der accepts) take the loop-form kernel
-// k_rsa_verify_big with L = ceil((bits + 2) / 28) <= RSA_L4096 limbs chosen per
-// key at run time (a fully expanded 3072-bit class, L = 110, took 28 minutes
-// to compile).
+// k_rsa_verify_big with L = ceil((8 k + 2) / 28) limbs (k = byte length of n)
+// rounded up to a multiple of RSA_BIG_ROWS (its Montgomery product runs that
+// many rows per pass), chosen per key at run time (a fully expanded 3072-bit
+// class, L = 110, took 28 minutes to compile).
 #define RSA_L1024 37
 #define RSA_L2048 74
 #define RSA_L4096 147
-#define RSA_LMAX RSA_L4096
+#ifndef RSA_BIG_ROWS
+#define RSA_BIG_ROWS 8
+#endif
+#define RSA_LMAX (((RSA_L4096 + RSA_BIG_ROWS - 1) / RSA_BIG_ROWS) * RSA_BIG_ROWS)
 
 // an inactive entry of a wave-padded record list (k_rsa_scatter)
 #define RSA_PAD 0xffffffffu

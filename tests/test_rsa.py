@@ -72,6 +72,36 @@ def test_host_der_parser_matches_oracle(rv):
         assert int.from_bytes(mod, "big") == n and ee == e, u["name"]
 
 
+def test_big_class_montgomery_rows_on_host():
+    """The loop-form class's Montgomery product (cess_amd/csrc/rsa_mont.hpp,
+    RSA_BIG_ROWS rows per pass as a systolic chain) compiled for the host:
+    a b R^-1 mod n, below 2n, 28-bit digits, for moduli of 2049-4096 bits and
+    operands up to 2n - 1, with the host's padded limb count (multiple of 8)."""
+    import ctypes
+    import subprocess
+    src = os.path.join(ROOT, "tests", "hostemu", "rsa_mont_emu.cpp")
+    lib = os.path.join(ROOT, "tests", "hostemu", "librsa_mont_emu.so")
+    hdr = os.path.join(ROOT, "cess_amd", "csrc", "rsa_mont.hpp")
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-DCESS_HOSTEMU", "-shared", "-fPIC", src, "-o", lib])
+    emu = ctypes.CDLL(lib)
+    M = (1 << 28) - 1
+    rng = random.Random(0x4d4f4e54)
+    for trial in range(200):
+        bits = rng.choice([2049, 2071, 2500, 3001, 3072, 4095, 4096])
+        n = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        kb = (bits + 7) // 8
+        L = ((8 * kb + 2 + 27) // 28 + 7) // 8 * 8        # host_rsa.cpp size_class_limbs
+        ninv = (-pow(n, -1, 1 << 28)) % (1 << 28)
+        a, b = (2 * n - 1, 2 * n - 1) if trial % 10 == 0 else (rng.randrange(2 * n), rng.randrange(2 * n))
+        arr = lambda v: (ctypes.c_uint32 * (L + 1))(*[(v >> (28 * i)) & M for i in range(L)] + [0])
+        out = (ctypes.c_uint32 * (L + 1))()
+        emu.emu_rsa_mont(arr(a), arr(b), arr(n), ctypes.c_uint32(ninv), L, out)
+        got = sum(out[i] << (28 * i) for i in range(L + 1))
+        assert all(out[i] <= M for i in range(L + 1)), (trial, bits)
+        assert got < 2 * n and got % n == a * b * pow(1 << (28 * L), -1, n) % n, (trial, bits)
+
+
 def _gpu_ctx():
     from cess_amd import bls
     return bls.Context(max_batch=4096)

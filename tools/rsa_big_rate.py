@@ -1,7 +1,7 @@
 """Throughput of the loop-form RSA class (2049-4096-bit moduli, k_rsa_verify_big)
 on one MI355X: the fixture's valid signatures under the 3072- and 4096-bit keys
 (tests/golden/rsa_vectors.json) replicated to a batch, device-resident records,
-codes checked against the fixture.  Usage (GPU box): python tools/rsa_big_rate.py"""
+codes checked against the fixture.  Usage (GPU box): python tools/rsa_big_rate.py [records]"""
 import json
 import os
 import sys
@@ -14,11 +14,12 @@ sys.path.insert(0, ROOT)
 from cess_amd import bls  # noqa: E402
 
 rv = json.load(open(os.path.join(ROOT, "tests", "golden", "rsa_vectors.json")))
-ctx = bls.Context(max_batch=1 << 16)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
+ctx = bls.Context(max_batch=N)
 for bits in (2048, 3072, 4096):
     ki = next(i for i, k in enumerate(rv["keys"]) if k["bits"] == bits and k["e"] == 65537)
     pool = [c for c in rv["cases"] if c["key"] == ki and c["code"] == 0]
-    n = 1 << 16
+    n = N
     recs = [pool[i % len(pool)] for i in range(n)]
     S = b"".join(bytes.fromhex(r["sig"]) for r in recs)
     M = b"".join(bytes.fromhex(r["msg"]) for r in recs)

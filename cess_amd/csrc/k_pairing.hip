@@ -38,7 +38,24 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
     const uint32_t* b = pair ? h_aff : sig_aff;
     return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
   };
-  auto src = [&](int pair, int k) { return pair ? ld_coeff4(coeffs, cstride, cj, k) : ld_coeff_uniform(neg_g2, k); };
+  // per-signature rows are read once: non-temporal loads, so the stream does
+  // not evict the G1 points the lines re-read from L2 (keyed tables, shared by
+  // many lanes, stay cached): k_miller 157.3 -> 152.9 ms per 1 M, counted
+  // traffic 27.8 -> 21.2 KB/sig (profiles/round3_al_sweep.txt)
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  auto ld_nt = [&](int k) {
+    coeff3 r;
+    uint32_t* w = &r.c0.c0.v[0];
+#pragma unroll
+    for (int q = 0; q < 18; q++) {
+      const u4v x = __builtin_nontemporal_load((const u4v*)(coeffs + (uint64_t)(18 * k + q) * cstride + cj));
+      w[4 * q] = x.x, w[4 * q + 1] = x.y, w[4 * q + 2] = x.z, w[4 * q + 3] = x.w;
+    }
+    return r;
+  };
+  auto src = [&](int pair, int k) {
+    return pair ? (cidx ? ld_coeff4(coeffs, cstride, cj, k) : ld_nt(k)) : ld_coeff_uniform(neg_g2, k);
+  };
   // cnorm (keyed batches): the key's lines were normalised to c2 = 1
   // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0.
   // (Per-signature rows are not normalised: k_norm_keys over every record

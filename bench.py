@@ -72,6 +72,9 @@ def parse():
                          "keyed: config[3] shape with per-signature verdicts; rsa: SURVEY §8(f) rank 4, RSA-2048 "
                          "PKCS#1 v1.5 raw verify (cp_enclave_verify::verify_rsa) over 32-byte messages; sign: SURVEY §8(f) "
                          "rank 3, batch PrivateKey::sign")
+    ap.add_argument("--host-steps", type=int, default=2,
+                    help="N=1 persig: extra steps from host buffers (cess_bls_verify_batch incl. PCIe), reported as "
+                         "host_buffers_sigs_per_s beside the device-resident value (0: skip)")
     ap.add_argument("--keys", type=int, default=16, help="distinct keys (rlc / keyed modes)")
     ap.add_argument("--forged-count", type=int, default=0, help="forgeries per rank (rlc mode)")
     ap.add_argument("--dry-run", action="store_true",
@@ -420,6 +423,9 @@ def run_rsa(args, ctx, rank, world):
             "config": {"workload": f"SURVEY §8(f) rank 4, cp_enclave_verify::verify_rsa: {n} sigs per GPU, inputs in HBM",
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
+            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
+            "host_buffers": host_rate,
+            "comm": comm,
             "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
             "roofline": {"bound": "valu-int", "kernel": "k_rsa_verify_2048u",
                          "achieved": achieved / 1e12, "peak": PEAK_MADS / 1e12,
@@ -508,6 +514,9 @@ def run_sign(args, ctx, rank, world):
             "config": {"workload": f"SURVEY §8(f) rank 3, batch PrivateKey::sign: {n} records per GPU",
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
+            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
+            "host_buffers": host_rate,
+            "comm": comm,
             "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
             "roofline": {"bound": "valu-int", "kernel": "k_sign", "achieved": achieved / 1e12,
                          "peak": PEAK_MADS / 1e12, "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
@@ -608,7 +617,10 @@ def run_rlc(args, ctx, rank, world):
             "config": {"workload": f"BASELINE config[3] shape: {n} sigs per GPU, {args.keys} distinct keys, "
                                    f"{args.forged_count} forged per GPU, RLC + Gt-partial RCCL all-gather + bisection",
                        "timing": "host-buffer API incl. key dedup and PCIe", "parallelism": f"shard-by-index x{world}"},
-            "verdicts_ok": ok, "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
+            "verdicts_ok": ok,
+            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
+            "host_buffers": host_rate,
+            "comm": comm, "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
             "runtime": runtime_provenance(),
         }), flush=True)
 
@@ -720,6 +732,29 @@ def main():
     words = np.frombuffer(ctx.from_device(d_bitmap, world * wpr * 8), dtype=np.uint64)
     popcount = int(np.unpackbits(words.view(np.uint8)).sum())
     ok = local_ok if world == 1 else ctx.comm_max(0.0 if local_ok else 1.0) == 0.0
+    # what the communicator itself reports (collective: every rank asks)
+    comm = None
+    if world > 1:
+        ci = ctx.comm_info()
+        comm = {"kind": ctx.comm_kind, "nranks": ci["nranks"], "rank": ci["rank"], "bus_ids": ci["bus_ids"],
+                "distinct_devices": len(set(ci["bus_ids"]))}
+        assert ci["nranks"] == world, (ci, world)
+
+    # the same records from HOST buffers (cess_bls_verify_batch: H2D copies,
+    # the pipeline, D2H of codes + bitmap), as node callers pass them; reported
+    # beside the device-resident `value`, never as it
+    host_rate = None
+    if world == 1 and args.mode == "persig" and args.host_steps > 0:
+        o_host = np.arange(n + 1, dtype=np.uint64) * 32
+        ctx.synchronize()
+        th = time.perf_counter()
+        for _ in range(args.host_steps):
+            hc, _hw = ctx.verify_fixed(S, P, M, o_host)
+        th = time.perf_counter() - th
+        host_rate = {"sigs_per_s": n * args.host_steps / th, "steps": args.host_steps,
+                     "ms_per_step": th / args.host_steps * 1e3,
+                     "codes_ok": bool((np.frombuffer(hc, dtype=np.uint8) == expect).all())}
+        ctx.stage_stats(reset=True)
 
     if rank == 0:
         total = n_total * args.steps
@@ -784,6 +819,9 @@ def main():
                        "ranks_share_gpu0": bool(args.one_device and world > 1),
                        "launch_chunk": chunk},
             "verdicts_ok": ok,
+            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
+            "host_buffers": host_rate,
+            "comm": comm,
             "bitmap_popcount": popcount,
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "stage_launches_per_step": {k: v / args.steps for k, v in launches_of.items()},

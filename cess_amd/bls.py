@@ -47,7 +47,8 @@ EXPORTS = (
     "cess_bls_stage_stats", "cess_bls_launch_records",
     # transport seam of the sharded entry points (RCCL or host shared memory)
     "cess_bls_comm_kind", "cess_bls_comm_shm_name", "cess_bls_comm_init_shm", "cess_bls_comm_open_shm",
-    "cess_bls_comm_close", "cess_bls_comm_agree", "cess_bls_comm_gather_verdicts",
+    "cess_bls_comm_close", "cess_bls_comm_agree", "cess_bls_comm_gather_verdicts", "cess_bls_comm_info",
+    "cess_bls_verify_batch_var_sharded",
     # node-side services: decode-only batches, the bounded verdict cache
     "cess_bls_deserialize_batch", "cess_bls_cache_create", "cess_bls_cache_destroy", "cess_bls_cache_clear",
     "cess_bls_cache_size", "cess_bls_cache_verify_var", "cess_bls_cache_insert_var", "cess_bls_sha256",
@@ -129,6 +130,9 @@ def load_library(path: str = LIB_PATH):
                                                           ctypes.POINTER(ctypes.c_int)]
         lib.cess_bls_comm_init_shm.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         lib.cess_bls_comm_kind.argtypes = [vp]
+        lib.cess_bls_comm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.c_char_p]
+        lib.cess_bls_verify_batch_var_sharded.argtypes = [vp, sz, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p, _u8p, _u64p]
         lib.cess_bls_comm_kind.restype = ctypes.c_char_p
         lib.cess_bls_comm_shm_name.argtypes = [ctypes.c_char_p]
         lib.cess_bls_comm_open_shm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
@@ -417,8 +421,37 @@ class Context:
                                                           bitmap))
         return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64]
 
+    def verify_var_sharded(self, records) -> Tuple[bytes, list]:
+        """Every rank passes the whole batch of (sig, msg, key) triples of any
+        lengths; returns the verdicts of all records (cess_bls_verify_batch_var_sharded)."""
+        n = len(records)
+        sigs = [bytes(r[0]) for r in records]
+        msgs = [bytes(r[1]) for r in records]
+        keys = [bytes(r[2]) for r in records]
+        codes = (ctypes.c_uint8 * max(n, 1))()
+        bitmap = (ctypes.c_uint64 * max((n + 63) // 64, 1))()
+        self._chk(self._lib.cess_bls_verify_batch_var_sharded(
+            self._h, n, _buf(b"".join(sigs)), _offsets([len(x) for x in sigs]), _buf(b"".join(keys)),
+            _offsets([len(k) for k in keys]), _buf(b"".join(msgs)), _offsets([len(m) for m in msgs]), codes, bitmap))
+        return bytes(codes)[:n], list(bitmap)[: (n + 63) // 64]
+
+    def comm_info(self, bus_ids: bool = True) -> dict:
+        """What the communicator reports: its rank count and this rank
+        (ncclCommCount / ncclCommUserRank over RCCL) and, when bus_ids (a
+        collective: pass it on every rank), every rank's GPU PCI bus id."""
+        nr, rk = ctypes.c_int(), ctypes.c_int()
+        buf = ctypes.create_string_buffer(32 * max(self.nranks if hasattr(self, "nranks") else 1, 1)) \
+            if bus_ids else None
+        self._chk(self._lib.cess_bls_comm_info(self._h, ctypes.byref(nr), ctypes.byref(rk), buf))
+        out = {"nranks": nr.value, "rank": rk.value}
+        if bus_ids:
+            raw = buf.raw
+            out["bus_ids"] = [raw[32 * q:32 * q + 32].split(b"\0", 1)[0].decode() for q in range(nr.value)]
+        return out
+
     def verify_sharded_device(self, n_total, d_sigs, d_pks, d_msgs, d_offs, d_codes_all, d_bitmap_all, stream=0):
-        """Device-resident sharded batch (this rank's shard in HBM); not synchronised."""
+        """Device-resident sharded batch (this rank's shard in HBM); returns
+        after the final status agreement (every rank sees any rank's failure)."""
         self._chk(self._lib.cess_bls_verify_batch_sharded_device(self._h, n_total, d_sigs, d_pks, d_msgs, d_offs,
                                                                  d_codes_all or None, d_bitmap_all, stream or None))
 

@@ -40,6 +40,13 @@ struct Transport {
   // Element-wise maximum over ranks of n host values, in place.
   virtual int max_i64(int64_t* v, int n) = 0;
   virtual int max_f64(double* v) = 0;
+  // What the communicator itself reports (RCCL: ncclCommCount /
+  // ncclCommUserRank; shm: the segment's rank count and this rank).
+  virtual int comm_count(int* count, int* my_rank) {
+    *count = nranks;
+    *my_rank = rank;
+    return CESS_BLS_OK;
+  }
 };
 
 // POSIX shared-memory transport (comm_shm.cpp).  `name` (from
@@ -60,6 +67,11 @@ int gather_verdicts(Transport& t, uint64_t n, const uint8_t* shard_codes, uint8_
 
 // every rank passed the same value (one collective step)
 int same_on_all_ranks(Transport& t, uint64_t v, bool* same);
+
+// Bounded waits of both transports: CLOCK_MONOTONIC in ms, and the deadline
+// of one wait, env CESS_BLS_COMM_TIMEOUT_MS (default 300 s)
+double comm_now_ms();
+double comm_timeout_ms();
 
 // shard of a batch for rank r of R (whole bitmap words, equal word count per rank; host.cpp)
 void shard_of(uint64_t n, int nranks, int rank, uint64_t* begin, uint64_t* end, uint64_t* words_per_rank);

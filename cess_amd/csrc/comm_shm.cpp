@@ -30,6 +30,20 @@
 
 namespace cess_host {
 
+double comm_now_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+double comm_timeout_ms() {
+  if (const char* e = getenv("CESS_BLS_COMM_TIMEOUT_MS")) {
+    const double v = strtod(e, nullptr);
+    if (v > 0) return v;
+  }
+  return 300e3;
+}
+
 namespace {
 
 constexpr uint64_t kMagic = 0x434553535f534d31ull;   // "CESS_SM1"
@@ -50,19 +64,8 @@ static_assert(sizeof(ShmHeader) <= kHeaderBytes, "header page");
 static_assert(std::atomic<uint32_t>::is_always_lock_free && std::atomic<uint64_t>::is_always_lock_free,
               "process-shared atomics must be lock-free");
 
-double now_ms() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
-}
-
-double timeout_ms() {
-  if (const char* e = getenv("CESS_BLS_COMM_TIMEOUT_MS")) {
-    const double v = strtod(e, nullptr);
-    if (v > 0) return v;
-  }
-  return 300e3;
-}
+double now_ms() { return comm_now_ms(); }
+double timeout_ms() { return comm_timeout_ms(); }
 
 // spin briefly, then yield, then sleep: ranks may wait seconds for a peer's
 // verification to finish

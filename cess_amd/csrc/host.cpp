@@ -33,7 +33,7 @@ extern "C" const char* cess_bls_status_string(int s) {
     case CESS_BLS_E_BAD_KEY: return "public key does not deserialize (verify_bls would panic)";
     case CESS_BLS_E_BAD_SIG: return "signature does not deserialize (verify_bls would panic)";
     case CESS_BLS_E_NO_COMM: return "no communicator (cess_bls_comm_init / cess_bls_comm_init_shm)";
-    case CESS_BLS_E_COMM: return "shared-memory communicator failed (peer timeout or transport error)";
+    case CESS_BLS_E_COMM: return "communicator failed (peer timeout, or the communicator was aborted)";
     case CESS_RSA_E_UNSUPPORTED: return "RSA key not supported on the GPU (> 2048-bit, even modulus or non-NULL parameters): the caller's CPU path decides";
   }
   return "unknown status";

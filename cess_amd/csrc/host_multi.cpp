@@ -16,6 +16,8 @@
 //    split the same way across them, one host thread per device, each writing
 //    its verdicts straight into the caller's buffers (no collective needed in
 //    one address space).
+#include <unistd.h>
+
 #include <thread>
 
 #include "host.hpp"
@@ -43,14 +45,26 @@ int cess_gen_one(cess_bls_ctx* c, int kind, size_t n, const uint8_t* sks, const 
 // RCCL transport (comm.hpp): production, one process per GPU, xGMI
 // ---------------------------------------------------------------------------
 namespace {
+// Every RCCL call is bounded: the communicator is created NON-BLOCKING
+// (ncclCommInitRankConfig, blocking = 0) and each wait -- init, a collective's
+// enqueue, the control stream draining -- polls ncclCommGetAsyncError against
+// a deadline (CESS_BLS_COMM_TIMEOUT_MS, default 300 s, the shm transport's).
+// A dead or stuck peer therefore ends in ncclCommAbort and CESS_BLS_E_COMM on
+// this rank instead of a hang; an RCCL-reported error ends in ncclCommAbort
+// and CESS_BLS_E_RCCL.  After either, the transport is broken and every later
+// call returns CESS_BLS_E_COMM at once.
 class RcclTransport final : public Transport {
  public:
   ~RcclTransport() override {
-    if (ctl_) {
-      (void)hipSetDevice(dev_);
-      (void)hipStreamSynchronize(ctl_);
+    if (ctl_) (void)hipSetDevice(dev_);
+    if (comm_) {
+      // drain our own control work, then a bounded finalize; abort if the
+      // peers never complete it
+      int r = ctl_ ? wait_stream(ctl_) : CESS_BLS_OK;
+      if (!r && comm_) r = issue(ncclCommFinalize(comm_));
+      if (!r && comm_) (void)ncclCommDestroy(comm_);
+      comm_ = nullptr;   // (a failed wait aborted it already)
     }
-    if (comm_) (void)ncclCommDestroy(comm_);
     if (ctl_) (void)hipStreamDestroy(ctl_);
   }
   const char* kind() const override { return "rccl"; }
@@ -62,21 +76,29 @@ class RcclTransport final : public Transport {
     this->rank = rank;
     HIPCHK(hipSetDevice(dev_));
     HIPCHK(hipStreamCreateWithFlags(&ctl_, hipStreamNonBlocking));
-    NCCLCHK(ncclCommInitRank(&comm_, nranks, id, rank));
-    return CESS_BLS_OK;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_) (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+      return CESS_BLS_E_RCCL;
+    }
+    return wait_ready();
   }
 
   int allgather_dev(int dev, void* dbuf, size_t bytes, hipStream_t s) override {
     (void)dev;
+    if (!comm_) return CESS_BLS_E_COMM;
     char* b = static_cast<char*>(dbuf);
-    NCCLCHK(ncclAllGather(b + (size_t)rank * bytes, b, bytes, ncclUint8, comm_, s));
-    return CESS_BLS_OK;
+    return issue(ncclAllGather(b + (size_t)rank * bytes, b, bytes, ncclUint8, comm_, s));
   }
 
   // Host-side collectives run on the control stream after the context's
   // previous work (order_begin): RCCL then executes this communicator's
   // collectives in the order every rank issued them.
   int allgather_host(void* buf, size_t bytes) override {
+    if (!comm_) return CESS_BLS_E_COMM;
     HIPCHK(hipSetDevice(dev_));
     int r = order_begin(ctx_, ctl_);
     if (r) return r;
@@ -84,28 +106,83 @@ class RcclTransport final : public Transport {
     char* d = buf_.as<char>();
     char* h = static_cast<char*>(buf);
     if (bytes) HIPCHK(hipMemcpyAsync(d + (size_t)rank * bytes, h + (size_t)rank * bytes, bytes, hipMemcpyHostToDevice, ctl_));
-    NCCLCHK(ncclAllGather(d + (size_t)rank * bytes, d, bytes, ncclUint8, comm_, ctl_));
+    r = issue(ncclAllGather(d + (size_t)rank * bytes, d, bytes, ncclUint8, comm_, ctl_));
+    if (r) return r;
     if (bytes) HIPCHK(hipMemcpyAsync(h, d, (size_t)nranks * bytes, hipMemcpyDeviceToHost, ctl_));
-    HIPCHK(hipStreamSynchronize(ctl_));
+    r = wait_stream(ctl_);
+    if (r) return r;
     return order_end(ctx_, ctl_);
   }
 
   int max_i64(int64_t* v, int n) override { return allreduce_max(v, n, ncclInt64); }
   int max_f64(double* v) override { return allreduce_max(v, 1, ncclFloat64); }
 
+  int comm_count(int* count, int* my_rank) override {
+    if (!comm_) return CESS_BLS_E_COMM;
+    if (ncclCommCount(comm_, count) != ncclSuccess || ncclCommUserRank(comm_, my_rank) != ncclSuccess)
+      return CESS_BLS_E_RCCL;
+    return CESS_BLS_OK;
+  }
+
  private:
   template <class T>
   int allreduce_max(T* v, int n, ncclDataType_t t) {
+    if (!comm_) return CESS_BLS_E_COMM;
     HIPCHK(hipSetDevice(dev_));
     int r = order_begin(ctx_, ctl_);
     if (r) return r;
     if (buf_.ensure(std::max<size_t>(64, n * sizeof(T)))) return CESS_BLS_E_OOM;
     T* d = buf_.as<T>();
     HIPCHK(hipMemcpyAsync(d, v, n * sizeof(T), hipMemcpyHostToDevice, ctl_));
-    NCCLCHK(ncclAllReduce(d, d, n, t, ncclMax, comm_, ctl_));
+    r = issue(ncclAllReduce(d, d, n, t, ncclMax, comm_, ctl_));
+    if (r) return r;
     HIPCHK(hipMemcpyAsync(v, d, n * sizeof(T), hipMemcpyDeviceToHost, ctl_));
-    HIPCHK(hipStreamSynchronize(ctl_));
+    r = wait_stream(ctl_);
+    if (r) return r;
     return order_end(ctx_, ctl_);
+  }
+
+  // abort the communicator (releases kernels waiting on peers) and mark the
+  // transport broken (comm_ null: every later call returns CESS_BLS_E_COMM)
+  int fail(int status) {
+    if (comm_) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+    return status;
+  }
+  // result of an RCCL call on the non-blocking communicator
+  int issue(ncclResult_t r) {
+    if (r == ncclSuccess) return CESS_BLS_OK;
+    if (r == ncclInProgress) return wait_ready();
+    return fail(CESS_BLS_E_RCCL);
+  }
+  // Poll `done` (true: finished, or a status < 0 to fail with) and the
+  // communicator's asynchronous error until the deadline.
+  template <class Done>
+  int poll(Done&& done) {
+    const double t_end = comm_now_ms() + comm_timeout_ms();
+    for (int spins = 0;; spins++) {
+      ncclResult_t st = ncclInProgress;
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return fail(CESS_BLS_E_RCCL);
+      if (st != ncclSuccess && st != ncclInProgress) return fail(CESS_BLS_E_RCCL);
+      const int d = done(st);
+      if (d > 0) return CESS_BLS_OK;
+      if (d < 0) return fail(d);
+      if (comm_now_ms() > t_end) return fail(CESS_BLS_E_COMM);
+      if (spins > 256) usleep(spins > 4096 ? 200 : 20);
+    }
+  }
+  // the communicator's state leaves ncclInProgress (init, an enqueue, finalize)
+  int wait_ready() {
+    if (!comm_) return CESS_BLS_E_COMM;
+    return poll([](ncclResult_t st) { return st == ncclSuccess ? 1 : 0; });
+  }
+  // stream s drained while the communicator stays healthy
+  int wait_stream(hipStream_t s) {
+    if (!comm_) return CESS_BLS_E_COMM;
+    return poll([s](ncclResult_t) {
+      const hipError_t q = hipStreamQuery(s);
+      return q == hipSuccess ? 1 : q == hipErrorNotReady ? 0 : CESS_BLS_E_HIP;
+    });
   }
 
   int dev_ = 0;
@@ -164,6 +241,28 @@ extern "C" int cess_bls_comm_init_shm(cess_bls_ctx* c, int nranks, int rank, con
   return CESS_BLS_OK;
 }
 
+extern "C" int cess_bls_comm_info(cess_bls_ctx* c, int* nranks_out, int* rank_out, char* bus_ids_out) {
+  ENTRY(c);
+  if (!c->xport) return CESS_BLS_E_NO_COMM;
+  int nr = 0, rk = 0;
+  int r = c->xport->comm_count(&nr, &rk);
+  if (r) return r;
+  if (nranks_out) *nranks_out = nr;
+  if (rank_out) *rank_out = rk;
+  if (!bus_ids_out) return CESS_BLS_OK;
+  // collective: every rank's PCI bus id, gathered in rank order
+  std::vector<char> ids((size_t)c->nranks * CESS_BLS_BUS_ID_BYTES, 0);
+  char* mine = &ids[(size_t)c->rank * CESS_BLS_BUS_ID_BYTES];
+  const int st = hipDeviceGetPCIBusId(mine, CESS_BLS_BUS_ID_BYTES - 1, c->device) == hipSuccess ? CESS_BLS_OK
+                                                                                                 : CESS_BLS_E_HIP;
+  r = agree(*c->xport, st);
+  if (r) return r;
+  r = c->xport->allgather_host(ids.data(), CESS_BLS_BUS_ID_BYTES);
+  if (r) return r;
+  memcpy(bus_ids_out, ids.data(), ids.size());
+  return CESS_BLS_OK;
+}
+
 extern "C" const char* cess_bls_comm_kind(cess_bls_ctx* c) {
   return (c && c->xport) ? c->xport->kind() : "none";
 }
@@ -194,6 +293,31 @@ extern "C" int cess_bls_verify_batch_sharded(cess_bls_ctx* c, size_t n, const ui
   std::vector<uint8_t> codes(std::max<uint64_t>(m, 1), 0xff);
   if (st == CESS_BLS_OK && m)
     st = verify_host(c, m, sigs + 48 * b, pks + 96 * b, msgs, offs + b, nullptr, codes.data(), nullptr, nullptr);
+  int r = agree(t, st);
+  if (r) return r;
+  return gather_verdicts(t, n, codes.data(), codes_out, bitmap_out);
+}
+
+extern "C" int cess_bls_verify_batch_var_sharded(cess_bls_ctx* c, size_t n, const uint8_t* sig_data,
+                                                 const uint64_t* sig_offsets, const uint8_t* pk_data,
+                                                 const uint64_t* pk_offsets, const uint8_t* msgs,
+                                                 const uint64_t* msg_offsets, uint8_t* codes_out, uint64_t* bitmap_out) {
+  ENTRY(c);
+  if (!c->xport) return CESS_BLS_E_NO_COMM;
+  Transport& t = *c->xport;
+  uint64_t b, e, wpr;
+  shard_of(n, c->nranks, c->rank, &b, &e, &wpr);
+  const uint64_t m = e - b;
+  // the whole batch's offsets are validated on every rank (as the fixed form)
+  int st = CESS_BLS_OK;
+  if (!sig_offsets || !pk_offsets || !msg_offsets) st = CESS_BLS_E_INVALID_ARG;
+  for (uint64_t i = 0; st == CESS_BLS_OK && i < n; i++)
+    if (sig_offsets[i + 1] < sig_offsets[i] || pk_offsets[i + 1] < pk_offsets[i] || msg_offsets[i + 1] < msg_offsets[i])
+      st = CESS_BLS_E_INVALID_ARG;
+  std::vector<uint8_t> codes(std::max<uint64_t>(m, 1), CESS_BLS_CODE_UNAVAILABLE);
+  if (st == CESS_BLS_OK && m)
+    st = verify_var_host(c, m, sig_data, sig_offsets + b, pk_data, pk_offsets + b, msgs, msg_offsets + b, codes.data(),
+                         nullptr);
   int r = agree(t, st);
   if (r) return r;
   return gather_verdicts(t, n, codes.data(), codes_out, bitmap_out);
@@ -238,8 +362,11 @@ extern "C" int cess_bls_verify_batch_sharded_device(cess_bls_ctx* c, size_t n_to
   }
   if (r) {
     // past the agreement the peers are committed to the all-gathers: take part
-    // with a rejecting block (no verdict bit set) and report the failure here
+    // with a block that holds no verdict -- no bitmap bit, and every code of
+    // the shard CESS_BLS_CODE_UNAVAILABLE, so records this rank never verified
+    // cannot read as OK (0) from whatever the caller's buffer held
     (void)hipMemsetAsync(my_words, 0, wpr * 8, s);
+    if (d_codes_all) (void)hipMemsetAsync(codes, CESS_BLS_CODE_UNAVAILABLE, wpr * 64, s);
   }
   // (4)
   int g = t.allgather_dev(c->device, d_bitmap_all, wpr * 8, s);
@@ -247,9 +374,11 @@ extern "C" int cess_bls_verify_batch_sharded_device(cess_bls_ctx* c, size_t n_to
     const int g2 = t.allgather_dev(c->device, d_codes_all, wpr * 64, s);
     if (!g) g = g2;
   }
-  if (r) return r;
-  if (g) return g;
-  return order_end(c, s);
+  const int oe = order_end(c, s);
+  // (5) a second status agreement, ordered after the all-gathers (the
+  // transport's host collectives wait for the context's last stream): a
+  // failure on any rank after (3) is returned on every rank
+  return agree(t, r ? r : g ? g : oe);
 }
 
 extern "C" int cess_bls_verify_batch_rlc_sharded(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks,

@@ -119,13 +119,19 @@ bool parse_spki(const uint8_t* b, size_t n, std::vector<uint8_t>& mod, uint64_t&
   return parse_pkcs1(bits.v + 1, bits.len - 1, mod, e);
 }
 
-// limbs of the key's size class: the expanded 1024 / 2048-bit classes, or
-// (2049..4096 bits, k_rsa_verify_big) the least multiple of RSA_BIG_ROWS with
-// 28 L >= 8 k + 2, so that every bit of a k-byte signature has a limb (the
-// s < n check sees all of it) and R = 2^(28 L) >= 4n
+// limbs of the key's size class.  Every class must satisfy BOTH
+//   28 L >= bits + 2  (R = 2^(28 L) >= 4n) and
+//   28 L >= 8 k       (every bit of a k-byte signature has a limb, so the
+//                      s < n check sees all of it: a 1033-bit key has 130-byte
+//                      signatures, 1040 bits > 28 x 37, and s + 2^1036 would
+//                      otherwise pass as s)
+// The expanded 1024 / 2048-bit classes when they qualify, else the loop-form
+// class (k_rsa_verify_big): the least multiple of RSA_BIG_ROWS with
+// 28 L >= 8 k + 2, which implies both.
 int size_class_limbs(size_t bits, size_t k_bytes) {
-  if (bits + 2 <= 28 * RSA_L1024) return RSA_L1024;
-  if (bits + 2 <= 28 * RSA_L2048) return RSA_L2048;
+  auto fits = [&](int L) { return bits + 2 <= (size_t)28 * L && 8 * k_bytes <= (size_t)28 * L; };
+  if (fits(RSA_L1024)) return RSA_L1024;
+  if (fits(RSA_L2048)) return RSA_L2048;
   const int L0 = (int)((8 * k_bytes + 2 + 27) / 28);
   const int L = (L0 + RSA_BIG_ROWS - 1) / RSA_BIG_ROWS * RSA_BIG_ROWS;
   return L0 <= RSA_L4096 ? L : 0;
@@ -372,7 +378,7 @@ extern "C" int cess_rsa_parse_key(const uint8_t* der, size_t len, int format, ui
   if ((!der && len) || !n_len || !e_out) return CESS_BLS_E_INVALID_ARG;
   std::vector<uint8_t> mod;
   uint64_t e = 0;
-  bool unsup = false;
+  bool unsup = false;   // not reported here: parse_key answers "does the crate parse it" (cess_rsa.h)
   const bool ok = format == CESS_RSA_KEY_PKCS1 ? parse_pkcs1(der, len, mod, e) : parse_spki(der, len, mod, e, &unsup);
   if (!ok) return CESS_BLS_E_BAD_KEY;
   *n_len = mod.size();

@@ -47,7 +47,8 @@ extern "C" {
 #define CESS_BLS_E_BAD_SIG (-8)  /* cess_bls_enclave_verify_bls: the signature does not deserialize (the reference panics) */
 #define CESS_BLS_E_NO_COMM (-9)  /* a sharded entry point on a context without cess_bls_comm_init[_shm] */
 /* (-10 is CESS_RSA_E_UNSUPPORTED, include/cess_rsa.h) */
-#define CESS_BLS_E_COMM (-11)    /* shared-memory communicator: a peer timed out or the transport failed */
+#define CESS_BLS_E_COMM (-11)    /* communicator (RCCL or shm): a peer timed out (CESS_BLS_COMM_TIMEOUT_MS) or the
+                                    communicator was aborted; every later collective on it fails the same way */
 
 enum cess_bls_code {
   CESS_BLS_CODE_OK = 0,
@@ -64,6 +65,7 @@ enum cess_bls_code {
 #define CESS_BLS_GT_BYTES 576
 #define CESS_BLS_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define CESS_BLS_COMM_NAME_BYTES 64  /* cess_bls_comm_shm_name */
+#define CESS_BLS_BUS_ID_BYTES 32     /* cess_bls_comm_info: one NUL-padded PCI bus id per rank */
 
 typedef struct cess_bls_ctx cess_bls_ctx;
 
@@ -230,7 +232,12 @@ int cess_bls_rlc_finish(cess_bls_ctx* ctx, int global_ok, uint8_t* codes_out, ui
 /* ncclGetUniqueId on one rank (e.g. rank 0); the caller distributes the 128
  * bytes to every rank out of band. */
 int cess_bls_comm_id(uint8_t id_out[CESS_BLS_COMM_ID_BYTES]);
-/* ncclCommInitRank on the context's device (collective: every rank calls it). */
+/* RCCL communicator on the context's device (collective: every rank calls it).
+ * Created non-blocking (ncclCommInitRankConfig, blocking = 0); this call and
+ * every later wait on the communicator poll ncclCommGetAsyncError against a
+ * deadline, env CESS_BLS_COMM_TIMEOUT_MS (default 300000): a peer that never
+ * arrives (or stops answering) makes this rank abort the communicator
+ * (ncclCommAbort) and return CESS_BLS_E_COMM instead of hanging. */
 int cess_bls_comm_init(cess_bls_ctx* ctx, int nranks, int rank, const uint8_t id[CESS_BLS_COMM_ID_BYTES]);
 /* Records [*begin, *end) of rank's shard of an n-record batch: ceil(n/64)
  * bitmap words split into nranks equal runs of *words_per_rank words (the last
@@ -245,12 +252,23 @@ int cess_bls_shard_range(uint64_t n, int nranks, int rank, uint64_t* begin, uint
 int cess_bls_verify_batch_sharded(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks,
                                   const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* codes_out,
                                   uint64_t* bitmap_out);
+/* Sharded batch of arbitrary-length encodings (collective; the layout of
+ * cess_bls_verify_batch_var, every rank passes the WHOLE batch): what node
+ * callers holding &[u8] slices pass -- a wrong-length signature or key gets
+ * its SIG_LEN / PK_LEN code in the gathered verdicts. */
+int cess_bls_verify_batch_var_sharded(cess_bls_ctx* ctx, size_t n, const uint8_t* sig_data,
+                                      const uint64_t* sig_offsets, const uint8_t* pk_data,
+                                      const uint64_t* pk_offsets, const uint8_t* msgs,
+                                      const uint64_t* msg_offsets, uint8_t* codes_out, uint64_t* bitmap_out);
 /* Device-resident sharded batch (collective): d_sigs/d_pks/d_msgs/d_msg_offsets
  * hold only this rank's shard (cess_bls_shard_range; offsets shard-local,
  * shard_n + 1 entries).  d_bitmap_all (nranks * words_per_rank words) receives
  * the full batch bitmap; d_codes_all (nranks * words_per_rank * 64 bytes, may
- * be NULL) the full code array (bytes past n unspecified).  Enqueued on
- * `stream` (NULL: the context's), not synchronised. */
+ * be NULL) the full code array (bytes past n unspecified).  The work is
+ * enqueued on `stream` (NULL: the context's); the call returns after a final
+ * status agreement that waits for the all-gathers, so a failure on any rank
+ * (also one after the work was enqueued) is returned on EVERY rank, and the
+ * failing rank's gathered codes are CESS_BLS_CODE_UNAVAILABLE (no verdict). */
 int cess_bls_verify_batch_sharded_device(cess_bls_ctx* ctx, size_t n_total, const uint8_t* d_sigs,
                                          const uint8_t* d_pks, const uint8_t* d_msgs,
                                          const uint64_t* d_msg_offsets, uint8_t* d_codes_all,
@@ -269,6 +287,12 @@ int cess_bls_verify_batch_rlc_sharded(cess_bls_ctx* ctx, size_t n_shard, const u
 /* Control-plane helpers over the same communicator (collective). */
 int cess_bls_comm_barrier(cess_bls_ctx* ctx);
 int cess_bls_comm_max_f64(cess_bls_ctx* ctx, double* value);
+/* What the communicator itself reports: *nranks_out (RCCL: ncclCommCount),
+ * *rank_out (ncclCommUserRank); either may be NULL.  With bus_ids_out
+ * non-NULL (on EVERY rank: it is then a collective) it receives each rank's
+ * device PCI bus id (hipDeviceGetPCIBusId), CESS_BLS_BUS_ID_BYTES per rank in
+ * rank order -- so a caller can show that N ranks ran on N distinct GPUs. */
+int cess_bls_comm_info(cess_bls_ctx* ctx, int* nranks_out, int* rank_out, char* bus_ids_out);
 /* "rccl", "shm" or "none" (static string). */
 const char* cess_bls_comm_kind(cess_bls_ctx* ctx);
 

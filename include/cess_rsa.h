@@ -49,7 +49,11 @@ enum cess_rsa_code {
 
 /* Host-side DER parse (the key checks of rsa 0.8: n <= 4096 bits,
  * 2 <= e <= 2^33 - 1).  n_out (may be NULL) receives the big-endian modulus
- * (*n_len bytes).  CESS_BLS_E_BAD_KEY where from_public_key_der fails. */
+ * (*n_len bytes).  CESS_BLS_E_BAD_KEY where from_public_key_der fails.
+ * This reports ONLY whether the reference crate parses the key: a key it
+ * parses but the GPU kernels cannot verify (even or tiny modulus, SPKI
+ * AlgorithmIdentifier parameters other than NULL) returns CESS_BLS_OK here and
+ * CESS_RSA_E_UNSUPPORTED from cess_rsa_keys_load / cess_rsa_verify. */
 int cess_rsa_parse_key(const uint8_t* der, size_t len, int format, uint8_t* n_out, size_t n_cap, size_t* n_len,
                        uint64_t* e_out);
 

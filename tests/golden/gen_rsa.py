@@ -128,6 +128,33 @@ def main():
         add(f"k{ki}_msg_too_long", ki, bytes(kb - 10), s)
         em = b"\x00\x02" + b"\xff" * (kb - len(hw) - 3) + b"\x00" + hw
         add(f"k{ki}_bt02", ki, hw, pow(int.from_bytes(em, "big"), d, n).to_bytes(kb, "big"))
+    # moduli just above the 1024-bit class's limb span (37 x 28 = 1036 bits):
+    # 1033 / 1034-bit keys have k = 130-byte signatures (1040 bits), so a
+    # signature s + 2^1036 (>= n: SIG_RANGE) differs from a valid s only in bits
+    # the 1024-bit class has no limb for -- the host must route these keys to a
+    # class whose limbs cover all 8 k signature bits.  1032 bits (k = 129) is
+    # the largest key that stays in the 1024-bit class.  Own seed.
+    rng3 = random.Random(0x52534133)
+    for bits in (1033, 1034, 1032):
+        n, e, d = o.gen_key(bits, 65537, rng3)
+        keys.append({"n": n, "e": e, "d": d})
+        out_keys.append({"bits": n.bit_length(), "e": e, "spki": o.encode_spki(n, e).hex(),
+                         "pkcs1": o.encode_pkcs1(n, e).hex()})
+        ki = len(keys) - 1
+        kb = (n.bit_length() + 7) // 8
+        hw = b"hello world!"
+        s = o.sign_raw(n, d, hw)
+        add(f"k{ki}_hello_world", ki, hw, s)
+        m = bytes(rng3.randrange(256) for _ in range(32))
+        add(f"k{ki}_valid32", ki, m, o.sign_raw(n, d, m))
+        si = int.from_bytes(s, "big")
+        for top in (1036, 1037, 1039):
+            if si + (1 << top) < (1 << (8 * kb)):
+                add(f"k{ki}_sig_plus_2^{top}", ki, hw, (si + (1 << top)).to_bytes(kb, "big"))
+        add(f"k{ki}_sig_top_bit", ki, hw, (si | (1 << (8 * kb - 1))).to_bytes(kb, "big"))
+        add(f"k{ki}_sig_eq_n", ki, hw, n.to_bytes(kb, "big"))
+        add(f"k{ki}_sig_max", ki, hw, b"\xff" * kb)
+        add(f"k{ki}_flipped_sig", ki, hw, s[:-1] + bytes([s[-1] ^ 1]))
     doc = {"generator": "tests/golden/gen_rsa.py (oracle/rsa_oracle.py)",
            "codes": {"0": "OK", "1": "SIG_LEN", "2": "SIG_RANGE", "3": "MSG_LEN", "4": "MISMATCH"},
            "keys": out_keys, "cases": cases, "bad_keys": bad_keys,

@@ -47,6 +47,13 @@ def main():
         codes, words = ctx.verify_sharded(S, P, M, o)
         out[f"host_{case}"] = {"codes": codes.hex(), "words": [int(w) for w in words]}
 
+    # arbitrary-length records (wrong-length golden records in rank 1's shard)
+    parts = [bytes(data[f"var_{k}"]) for k in range(3)]
+    offs = [data[f"var_{k}_o"] for k in range(3)]
+    recs = [tuple(parts[k][int(offs[k][i]):int(offs[k][i + 1])] for k in range(3)) for i in range(len(offs[0]) - 1)]
+    codes, words = ctx.verify_var_sharded(recs)
+    out["var"] = {"codes": codes.hex(), "words": [int(w) for w in words]}
+
     # a failure on one rank (rank 1 corrupts its copy of the offsets inside its
     # shard) fails the call on EVERY rank, then the communicator still works
     S, P, M = bytes(data["a_S"]), bytes(data["a_P"]), bytes(data["a_M"])

@@ -231,3 +231,64 @@ def test_verify_batch_keeps_user_key_table(vectors):
         assert codes == v.codes
     finally:
         c.close()
+
+
+def test_comm_info_single_rank(comm_ctx):
+    """The communicator reports its own size and rank (ncclCommCount /
+    ncclCommUserRank) and the PCI bus id of each rank's device."""
+    info = comm_ctx.comm_info()
+    assert info["nranks"] == 1 and info["rank"] == 0
+    assert len(info["bus_ids"]) == 1 and ":" in info["bus_ids"][0]
+    assert comm_ctx.comm_info(bus_ids=False) == {"nranks": 1, "rank": 0}
+
+
+def test_var_sharded_single_rank(ctx, comm_ctx, vectors):
+    """Arbitrary-length records through the sharded var entry point: the
+    wrong-length golden records get their SIG_LEN / PK_LEN codes."""
+    sigs, msgs, pks = _signed(ctx, 600, 44)
+    recs = list(zip(sigs, msgs, pks))
+    fx = [(bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"]), c["code"])
+          for c in vectors["length_cases"] + vectors["cases"]]
+    for j, (s, m, k, _) in enumerate(fx):
+        recs.insert(7 * j + 3, (s, m, k))
+    expect = [0] * len(recs)
+    for j, f in enumerate(fx):
+        expect[7 * j + 3] = f[3]
+    codes, words = comm_ctx.verify_var_sharded(recs)
+    assert list(codes) == expect
+    assert {1, 3} <= set(codes)
+    assert words == [sum(1 << b for b in range(64) if w * 64 + b < len(recs) and codes[w * 64 + b] == 0)
+                     for w in range((len(recs) + 63) // 64)]
+
+
+LONE_RANK = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+from cess_amd import bls
+bls.load_library()
+c = bls.Context(max_batch=256)
+t0 = time.time()
+try:
+    c.comm_init(2, 0, bls.comm_id())      # rank 1 never arrives
+    print("STATUS 0", time.time() - t0)
+except bls.BlsInfraError as ex:
+    print("STATUS", ex.status, time.time() - t0)
+c.close()
+"""
+
+
+def test_rccl_lone_rank_fails_within_deadline():
+    """A rank whose peer never arrives: the non-blocking RCCL init is polled
+    against CESS_BLS_COMM_TIMEOUT_MS, aborted, and returns CESS_BLS_E_COMM --
+    a non-zero exit instead of a hang in the first 8-GPU run."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CESS_BLS_COMM_TIMEOUT_MS="4000", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, "-c", LONE_RANK, root], env=env, capture_output=True, text=True, timeout=100)
+    line = [x for x in p.stdout.splitlines() if x.startswith("STATUS")]
+    assert p.returncode == 0 and line, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    _, st, dt = line[-1].split()
+    assert int(st) == bls.E_COMM, line
+    assert 3.5 < float(dt) < 60, line

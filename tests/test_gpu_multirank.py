@@ -15,9 +15,16 @@ refuses two ranks on one device) and run
     forgeries on rank 1;
   * a failure on one rank only (corrupt offsets; a missing device buffer):
     every rank must return the failure (no hang), and the next call works.
-The gathered codes and bitmaps must equal a single-context run of the same
-records bit-exactly, on both ranks.  Reference axis: one verdict per
-(sig, msg, key) as verify_bls_signature (utils/verify-bls-signatures/src/lib.rs:243).
+  * cess_bls_verify_batch_var_sharded with the wrong-length golden records
+    (SIG_LEN / PK_LEN) in rank 1's shard.
+Expected codes come from the CONSTRUCTION, not from the product: a record
+signed by the library's sign kernel (pinned by the reference's sign KAT) is 0,
+a forgery 5, an injected golden record its fixture code (every fixed-length
+golden case: non-subgroup, off-curve, x >= p, bad flags, the (O, O) identity
+pairs, precedence).  The gathered codes and bitmaps must equal them on both
+ranks, and a single-context run must equal them too.  Reference axis: one
+verdict per (sig, msg, key) as verify_bls_signature
+(utils/verify-bls-signatures/src/lib.rs:243-246).
 """
 import json
 import os
@@ -56,16 +63,25 @@ def _offs(msgs):
 
 
 def _rank1_adversarial(vectors, sigs, msgs, pks, lo, seed):
-    """forgeries + fixed-length adversarial golden records at indices >= lo (rank 1's shard)"""
+    """Every fixed-length golden record plus 10 forgeries at indices >= lo
+    (rank 1's shard); returns the records and their codes by construction."""
     rng = random.Random(seed)
     cases = [c for c in vectors["cases"] if len(c["sig"]) == 96 and len(c["pk"]) == 192]
-    idx = rng.sample(range(lo, len(sigs)), 40)
-    for j, i in enumerate(idx[:30]):
-        c = cases[j % len(cases)]
+    assert any(c["name"].startswith("identity_pair") for c in cases)      # (O, O) records among them
+    idx = rng.sample(range(lo, len(sigs)), len(cases) + 10)
+    expect = [0] * len(sigs)
+    for c, i in zip(cases, idx):
         sigs[i], msgs[i], pks[i] = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
-    for i in idx[30:]:
+        expect[i] = c["code"]
+    for i in idx[len(cases):]:
         msgs[i] = bytes(b ^ 0x5A for b in msgs[i])      # forgeries
-    return sigs, msgs, pks
+        expect[i] = 5
+    return sigs, msgs, pks, bytes(expect)
+
+
+def _words(codes):
+    n = len(codes)
+    return [sum(1 << b for b in range(64) if 64 * w + b < n and codes[64 * w + b] == 0) for w in range((n + 63) // 64)]
 
 
 def _arr(b):
@@ -78,13 +94,28 @@ def multirank(ctx, vectors, tmp_path_factory):
     data, expect = {}, {}
     for case, n in (("a", 1000), ("b", 4096 + 5)):
         lo = bls.shard_range(n, WORLD, 1)[0]
-        sigs, msgs, pks = _rank1_adversarial(vectors, *_signed(ctx, n, 40 + n), lo=lo, seed=n)
+        sigs, msgs, pks, want = _rank1_adversarial(vectors, *_signed(ctx, n, 40 + n), lo=lo, seed=n)
         S, P, M, o = b"".join(sigs), b"".join(pks), b"".join(msgs), _offs(msgs)
         codes, words = ctx.verify_fixed(S, P, M, o)
-        assert set(codes[:lo]) == {0} and len(set(codes[lo:])) >= 4   # the bad records are all in rank 1's shard
+        assert codes == want and words == _words(want)       # single context vs construction
+        assert set(want[:lo]) == {0} and len(set(want[lo:])) >= 5   # the bad records are all in rank 1's shard
         data.update({f"{case}_S": _arr(S), f"{case}_P": _arr(P), f"{case}_M": _arr(M), f"{case}_o": o,
                      f"{case}_n": np.uint64(n)})
-        expect[case] = (codes, words)
+        expect[case] = (want, _words(want))
+        if case == "a":
+            # the var-length batch: case a's records with the wrong-length golden
+            # records inserted into rank 1's shard
+            recs = list(zip(sigs, msgs, pks))
+            vw = list(want)
+            for j, c in enumerate(vectors["length_cases"]):
+                at = len(recs) - 3 - 37 * j
+                recs.insert(at, (bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])))
+                vw.insert(at, c["code"])
+            assert bls.shard_range(len(recs), WORLD, 1)[0] < len(recs) - 3 - 37 * 6
+            for k, part in enumerate(zip(*recs)):
+                data[f"var_{k}"] = _arr(b"".join(part))
+                data[f"var_{k}_o"] = _offs(part)
+            expect["var"] = (bytes(vw), _words(vw))
     for r, n in ((0, 1500), (1, 1700)):
         sigs, msgs, pks = _signed(ctx, n, 60 + r, keys=3)
         if r == 1:
@@ -92,7 +123,9 @@ def multirank(ctx, vectors, tmp_path_factory):
             msgs[1600] = bytes(31) + b"\x01"
         S, P, M, o = b"".join(sigs), b"".join(pks), b"".join(msgs), _offs(msgs)
         data.update({f"rlc{r}_S": _arr(S), f"rlc{r}_P": _arr(P), f"rlc{r}_M": _arr(M), f"rlc{r}_o": o})
-        expect[f"rlc{r}"] = ctx.verify_fixed(S, P, M, o)
+        want = bytes(5 if (r == 1 and i in (17, 1600)) else 0 for i in range(n))
+        assert ctx.verify_fixed(S, P, M, o) == (want, _words(want))
+        expect[f"rlc{r}"] = (want, _words(want))
     path = str(tmp / "data.npz")
     np.savez(path, **data)
     name = bls.comm_shm_name()
@@ -123,7 +156,7 @@ def test_transport_is_shm(multirank):
 
 
 @pytest.mark.parametrize("case", ["a", "b"])
-def test_host_sharded_equals_single_context(multirank, case):
+def test_host_sharded_equals_construction(multirank, case):
     out, expect = multirank
     codes, words = expect[case]
     for o in out:
@@ -131,7 +164,16 @@ def test_host_sharded_equals_single_context(multirank, case):
         assert o[f"host_{case}"]["words"] == words
 
 
-def test_device_sharded_equals_single_context(multirank):
+def test_var_sharded_wrong_lengths(multirank):
+    out, expect = multirank
+    codes, words = expect["var"]
+    assert {1, 3} <= set(codes)
+    for o in out:
+        assert bytes.fromhex(o["var"]["codes"]) == codes
+        assert o["var"]["words"] == words
+
+
+def test_device_sharded_equals_construction(multirank):
     out, expect = multirank
     codes, words = expect["b"]
     for o in out:

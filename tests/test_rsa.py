@@ -196,9 +196,9 @@ def test_gpu_device_batch_many(rv, extra_keys):
     table -> the unsorted lists and k_rsa_verify_2048."""
     from cess_amd import bls
     rng = random.Random(11)
-    keys = [k for k in rv["keys"] if k["bits"] <= 2048]
+    keys = [k for k in rv["keys"] if k["bits"] in (1024, 2048)]      # the expanded classes only
     parsed = [o.parse_spki(bytes.fromhex(k["spki"])) for k in keys]
-    base = [x for x in rv["cases"] if rv["keys"][x["key"]]["bits"] <= 2048]
+    base = [x for x in rv["cases"] if rv["keys"][x["key"]]["bits"] in (1024, 2048)]
     kmap = {rv["keys"].index(k): j for j, k in enumerate(keys)}
     recs = []
     for _ in range(3000):

@@ -150,11 +150,14 @@ pub trait GpuVerify {
 pub mod runtime {
     use super::*;
 
-    /// Drop-in for `cp_enclave_verify::verify_bls(key, msg, sig)`.
-    pub fn verify_bls(key: &[u8], msg: &[u8], sig: &[u8]) -> bool {
+    /// Drop-in for `cp_enclave_verify::verify_bls(key, msg, sig) -> Result<(), ()>`
+    /// (primitives/enclave-verify/src/lib.rs:230): same signature, so the
+    /// reference's call sites (and c-pallets/audit, patches/cess-gpu-verify.patch)
+    /// use it unchanged.
+    pub fn verify_bls(key: &[u8], msg: &[u8], sig: &[u8]) -> Result<(), ()> {
         match gpu_verify::verify_bls(key, msg, sig) {
-            HOOK_TRUE => true,
-            HOOK_FALSE => false,
+            HOOK_TRUE => Ok(()),
+            HOOK_FALSE => Err(()),
             _ => cp_enclave_verify::verify_bls(key, msg, sig),
         }
     }

@@ -154,8 +154,16 @@ def comm_setup(ctx, rank: int, world: int, transport: str = "rccl"):
     if rank == 0:
         rdv_put("comm_id", bls.comm_id())
     cid = rdv_get("comm_id")
-    ctx.comm_init(world, rank, cid)
-    ctx.comm_barrier()
+    try:
+        ctx.comm_init(world, rank, cid)
+        ctx.comm_barrier()
+    except bls.BlsInfraError as ex:
+        # a peer never arrived (CESS_BLS_COMM_TIMEOUT_MS) or RCCL failed: exit
+        # non-zero at once.  _exit, because a rank whose RCCL bootstrap never
+        # completed keeps a helper thread blocked inside RCCL (include/cess_bls.h)
+        print(json.dumps({"error": "communicator", "status": ex.status, "rank": rank, "message": str(ex)}),
+              file=sys.stderr, flush=True)
+        os._exit(3)
     rdv_cleanup(rank, world)
 
 

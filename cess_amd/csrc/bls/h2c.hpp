@@ -6,8 +6,9 @@
 //   expand_message_xmd (SHA-256; the 64-byte Z_pad block is a constant midstate;
 //   b1..b4 share a constant second block) -> u0, u1 = OS2IP(64 B) mod p
 //   -> simplified SWU on E' (RFC 9380 App. F.2 straight-line, sqrt_ratio for p = 3 mod 4)
-//   -> 11-isogeny evaluated homogeneously (no inversion) -> Q0 + Q1
-//   -> clear_cofactor [1 - x] -> one inversion to affine.
+//   -> Q0 + Q1 on E' (complete addition) -> ONE 11-isogeny evaluation
+//   -> clear_cofactor [1 - x] (Jacobian ladder, complete-formula recompute
+//   for the lanes that end with Z = 0) -> affine.
 #pragma once
 #include "curve.hpp"
 
@@ -191,50 +192,117 @@ CESS_HD void map_to_curve_sswu(const fp& u, fp& xn, fp& xd, fp& y) {
   xd = tv4;
 }
 
-// 11-isogeny E' -> E, homogeneous output (X : Y : Z).
-// The four rational-map polynomials are evaluated together by homogeneous
-// Horner steps in (xn : xd), all padded to degree 15:
-//   H_P = sum_i k_i xn^i xd^(15-i),  acc_i = acc_(i+1) xn + k_i xd^(15-i),
-// so XN' = XNUM_h xd^4 and XD' = XDEN_h xd^5 = (XDEN_h xd) xd^4 carry the same
-// factor and the point (XN' YD : y YN XD' : XD' YD) is the textbook one scaled
-// by xd^4 (xd != 0 by SSWU).  Live state: four accumulators, xd^(15-i), xn,
-// xd, y -- instead of 32 tabulated powers (384 dwords, which spilled).
-// 121 multiplies vs 140 for the tabulated form.
-CESS_HD g1p iso_map(const fp& xn, const fp& xd, const fp& y) {
+// 11-isogeny E' -> E on a homogeneous projective point (X : Y : Z) of E'
+// (x = X/Z, y = Y/Z).  The four rational-map polynomials are evaluated
+// together by homogeneous Horner steps in (X : Z), all padded to degree 15:
+//   H_P = sum_i k_i X^i Z^(15-i),  acc_i = acc_(i+1) X + k_i Z^(15-i),
+// so XN' = XNUM_h Z^4 and XD' = XDEN_h Z^5 = (XDEN_h Z) Z^4 carry the same
+// factor, and the image is (XN' YD Z : Y YN XD' : XD' YD Z) -- the textbook
+// point scaled by Z^5 (Z != 0 here: the caller maps O' to O itself).  Live
+// state: four accumulators, Z^(15-i), X, Z, Y -- instead of 32 tabulated
+// powers (384 dwords, which spilled).
+CESS_HD g1p iso_map_proj(const fp& X, const fp& Y, const fp& Z) {
   fp aXN = fp_zero(), aXD = fp_zero(), aYN = fp_zero(), aYD = fp_zero(), D = fp_one();
 #pragma unroll 1
   for (int i = 15; i >= 0; i--) {
     if (i < 15) {
-      D = mul(D, xd);
-      aYN = mul(aYN, xn);
-      aYD = mul(aYD, xn);
-      if (i < 11) aXN = mul(aXN, xn);
-      if (i < 10) aXD = mul(aXD, xn);
+      D = mul(D, Z);
+      aYN = mul(aYN, X);
+      aYD = mul(aYD, X);
+      if (i < 11) aXN = mul(aXN, X);
+      if (i < 10) aXD = mul(aXD, X);
     }
     aYN = add(aYN, mul(fp_from(c::ISO_YNUM[i]), D));
     aYD = add(aYD, mul(fp_from(c::ISO_YDEN[i]), D));
     if (i <= 11) aXN = add(aXN, mul(fp_from(c::ISO_XNUM[i]), D));
     if (i <= 10) aXD = add(aXD, mul(fp_from(c::ISO_XDEN[i]), D));
   }
-  return {mul(aXN, aYD), mul(mul(y, aYN), aXD), mul(aXD, aYD)};
+  const fp yd = mul(aYD, Z);
+  return {mul(aXN, yd), mul(mul(Y, aYN), aXD), mul(aXD, yd)};
 }
 
-// hash_to_g1 up to the cofactor clearing (projective), one SSWU+isogeny copy
-CESS_HD g1p hash_to_g1_proj(const uint8_t* msg, uint32_t len) {
+// Complete addition on E': y^2 = x^3 + A'x + B' (a != 0), Renes-Costello-
+// Batina eprint 2015/1060 Alg. 1 (12M + 3 m_a + 2 m_3b): exact for every pair
+// of points, doubling and inverses included.
+CESS_HD g1p iso_curve_add(const g1p& p, const g1p& q) {
+  const fp A = fp_from(c::ISO_A), B3 = mul3(fp_from(c::ISO_B));
+  fp t0 = mul(p.x, q.x), t1 = mul(p.y, q.y), t2 = mul(p.z, q.z);
+  fp t3 = sub(mul(add_nr(p.x, p.y), add_nr(q.x, q.y)), add(t0, t1));
+  fp t4 = sub(mul(add_nr(p.x, p.z), add_nr(q.x, q.z)), add(t0, t2));
+  fp t5 = sub(mul(add_nr(p.y, p.z), add_nr(q.y, q.z)), add(t1, t2));
+  fp z3 = add(mul(B3, t2), mul(A, t4));
+  fp x3 = sub(t1, z3);
+  z3 = add(t1, z3);
+  fp y3 = mul(x3, z3);
+  t1 = add(dbl(t0), t0);
+  t2 = mul(A, t2);
+  t4 = mul(B3, t4);
+  t1 = add(t1, t2);
+  t2 = mul(A, sub(t0, t2));
+  t4 = add(t4, t2);
+  y3 = add(y3, mul(t1, t4));
+  x3 = sub(mul(t3, x3), mul(t5, t4));
+  z3 = add(mul(t5, z3), mul(t3, t1));
+  return {x3, y3, z3};
+}
+
+// [1 - x] R for an affine point R of E(Fp) (h_eff of RFC 9380 for G1),
+// 1 - x = 0xd201000000010001: a Jacobian ladder with mixed additions of R
+// (dbl-2009-l 2M + 5S against the complete projective doubling's 6M + 2S).
+// Those formulas are incomplete, but an exceptional step (T = +-R or O) needs
+// R of order dividing a number below 2^64, i.e. R with no component in G1,
+// and it leaves Z = 0, which stays 0: a lane that ends with Z = 0 recomputes
+// [1 - x]R with the complete formulas (divergent; never taken for a hash
+// output in practice), so the result is exact for every R.
+CESS_HD g1a clear_cofactor_g1(const fp& rx, const fp& ry) {
+  g1p acc = {rx, ry, fp_one()};
+#pragma unroll 1
+  for (int b = 62; b >= 0; b--) {
+    acc = jac_dbl(acc);
+    if ((H_EFF_G1 >> b) & 1u) acc = jac_add_mixed(acc, rx, ry);
+  }
+  if (is_zero(acc.z)) return proj_to_affine(proj_mul_u64_mixed(rx, ry, H_EFF_G1));
+  const fp iz = inv(acc.z), iz2 = sqr(iz);
+  g1a r;
+  r.inf = false;
+  r.x = mul(acc.x, iz2);
+  r.y = mul(acc.y, mul(iz2, iz));
+  return r;
+}
+
+// hash_to_g1 (RFC 9380 BLS12381G1_XMD:SHA-256_SSWU_RO_, the reference's
+// hash_to_g1 at src/lib.rs:25-31):
+//   * Q0 + Q1 is formed on E' (complete addition above) and the 11-isogeny
+//     applied ONCE: the isogeny is a group homomorphism, so iso(Q0 + Q1) =
+//     iso(Q0) + iso(Q1) -- one ~120-multiply map evaluation less;
+//   * the cofactor clearing is clear_cofactor_g1 (Jacobian ladder, complete
+//     recompute for the lanes that end with Z = 0).
+CESS_HD g1a hash_to_g1(const uint8_t* msg, uint32_t len) {
   uint32_t uni[32];
   expand_message_xmd_128(msg, len, uni);
-  g1p q[2];
+  // one SSWU body for both field elements; the sum accumulates in registers
+  // (an array q[2] indexed by the loop counter, or uni indexed by it, would
+  // live in scratch)
+  g1p s;
 #pragma unroll 1
   for (int j = 0; j < 2; j++) {
-    fp u = fp_from_be64_words(j ? uni + 16 : uni);
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = j ? uni[16 + k] : uni[k];
     fp xn, xd, y;
-    map_to_curve_sswu(u, xn, xd, y);
-    q[j] = iso_map(xn, xd, y);
+    map_to_curve_sswu(fp_from_be64_words(w), xn, xd, y);
+    const g1p q = {xn, mul(y, xd), xd};   // (xn/xd, y), xd != 0
+    s = j ? iso_curve_add(s, q) : q;
   }
-  g1p r = proj_add(q[0], q[1]);
-  return proj_mul_u64(r, H_EFF_G1);
+  g1a r;
+  r.inf = true;
+  r.x = fp_zero();
+  r.y = fp_one();
+  if (is_zero(s.z)) return r;   // Q0 = -Q1: the sum is O', its image O
+  const g1p t = iso_map_proj(s.x, s.y, s.z);
+  if (is_zero(t.z)) return r;   // s in the isogeny's kernel: image O
+  const fp zi = inv(t.z);
+  return clear_cofactor_g1(mul(t.x, zi), mul(t.y, zi));
 }
-
-CESS_HD g1a hash_to_g1(const uint8_t* msg, uint32_t len) { return proj_to_affine(hash_to_g1_proj(msg, len)); }
 
 }  // namespace bls

@@ -16,8 +16,12 @@
 //    split the same way across them, one host thread per device, each writing
 //    its verdicts straight into the caller's buffers (no collective needed in
 //    one address space).
+#include <stdio.h>
+#include <stdlib.h>
 #include <unistd.h>
 
+#include <atomic>
+#include <memory>
 #include <thread>
 
 #include "host.hpp"
@@ -53,6 +57,21 @@ namespace {
 // this rank instead of a hang; an RCCL-reported error ends in ncclCommAbort
 // and CESS_BLS_E_RCCL.  After either, the transport is broken and every later
 // call returns CESS_BLS_E_COMM at once.
+// env CESS_BLS_COMM_TRACE=1: timestamped trace of the transport's RCCL calls on stderr
+static bool comm_trace() {
+  static const bool on = getenv("CESS_BLS_COMM_TRACE") != nullptr;
+  return on;
+}
+#define CTRACE(...)                                                                   \
+  do {                                                                                \
+    if (comm_trace()) {                                                               \
+      fprintf(stderr, "[cess comm %.3f] ", comm_now_ms() * 1e-3);                      \
+      fprintf(stderr, __VA_ARGS__);                                                   \
+      fprintf(stderr, "\n");                                                          \
+      fflush(stderr);                                                                 \
+    }                                                                                 \
+  } while (0)
+
 class RcclTransport final : public Transport {
  public:
   ~RcclTransport() override {
@@ -76,10 +95,46 @@ class RcclTransport final : public Transport {
     this->rank = rank;
     HIPCHK(hipSetDevice(dev_));
     HIPCHK(hipStreamCreateWithFlags(&ctl_, hipStreamNonBlocking));
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
-    const ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
-    if (r != ncclSuccess && r != ncclInProgress) {
+    // RCCL's bootstrap blocks the calling thread until every rank has
+    // connected, even for a non-blocking communicator (measured on MI355X:
+    // ncclCommInitRankConfig never returned for a lone rank), so the call runs
+    // on a helper thread and this one waits for it against the deadline.  A
+    // helper that returns after the caller gave up aborts its communicator
+    // itself; one that never returns stays blocked in the bootstrap (detached:
+    // it holds only the shared job state).
+    struct InitJob {
+      std::atomic<int> state{0};   // 0 running, 1 returned, 2 abandoned by the caller
+      ncclComm_t comm = nullptr;
+      ncclResult_t res = ncclInternalError;
+    };
+    auto job = std::make_shared<InitJob>();
+    CTRACE("init rank %d of %d: ncclCommInitRankConfig (non-blocking) on a helper thread", rank, nranks);
+    std::thread([job, dev = dev_, nranks, rank, id]() {
+      (void)hipSetDevice(dev);
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      ncclComm_t comm = nullptr;
+      const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &cfg);
+      job->comm = comm;
+      job->res = r;
+      int running = 0;
+      if (!job->state.compare_exchange_strong(running, 1) && comm) (void)ncclCommAbort(comm);
+    }).detach();
+    const double t_end = comm_now_ms() + comm_timeout_ms();
+    for (int spins = 0; job->state.load() == 0; spins++) {
+      if (comm_now_ms() > t_end) {
+        int running = 0;
+        if (job->state.compare_exchange_strong(running, 2)) {
+          CTRACE("init: deadline passed with the bootstrap still waiting for peers");
+          return CESS_BLS_E_COMM;
+        }
+        break;   // it returned just now
+      }
+      if (spins > 256) usleep(spins > 4096 ? 1000 : 50);
+    }
+    comm_ = job->comm;
+    CTRACE("init returned %d", (int)job->res);
+    if (job->res != ncclSuccess && job->res != ncclInProgress) {
       if (comm_) (void)ncclCommAbort(comm_);
       comm_ = nullptr;
       return CESS_BLS_E_RCCL;
@@ -145,7 +200,9 @@ class RcclTransport final : public Transport {
   // abort the communicator (releases kernels waiting on peers) and mark the
   // transport broken (comm_ null: every later call returns CESS_BLS_E_COMM)
   int fail(int status) {
+    CTRACE("fail(%d): ncclCommAbort", status);
     if (comm_) (void)ncclCommAbort(comm_);
+    CTRACE("abort returned");
     comm_ = nullptr;
     return status;
   }
@@ -167,7 +224,10 @@ class RcclTransport final : public Transport {
       const int d = done(st);
       if (d > 0) return CESS_BLS_OK;
       if (d < 0) return fail(d);
-      if (comm_now_ms() > t_end) return fail(CESS_BLS_E_COMM);
+      if (comm_now_ms() > t_end) {
+        CTRACE("deadline passed (state %d)", (int)st);
+        return fail(CESS_BLS_E_COMM);
+      }
       if (spins > 256) usleep(spins > 4096 ? 200 : 20);
     }
   }

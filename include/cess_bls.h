@@ -237,7 +237,11 @@ int cess_bls_comm_id(uint8_t id_out[CESS_BLS_COMM_ID_BYTES]);
  * every later wait on the communicator poll ncclCommGetAsyncError against a
  * deadline, env CESS_BLS_COMM_TIMEOUT_MS (default 300000): a peer that never
  * arrives (or stops answering) makes this rank abort the communicator
- * (ncclCommAbort) and return CESS_BLS_E_COMM instead of hanging. */
+ * (ncclCommAbort) and return CESS_BLS_E_COMM instead of hanging.  RCCL's
+ * bootstrap blocks its calling thread until every rank connects, so the init
+ * runs on a helper thread; when THIS call times out that thread stays blocked
+ * inside RCCL, and the process should end with _exit() (static destructors
+ * may otherwise run under it). */
 int cess_bls_comm_init(cess_bls_ctx* ctx, int nranks, int rank, const uint8_t id[CESS_BLS_COMM_ID_BYTES]);
 /* Records [*begin, *end) of rank's shard of an n-record batch: ceil(n/64)
  * bitmap words split into nranks equal runs of *words_per_rank words (the last

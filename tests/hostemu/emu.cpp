@@ -51,6 +51,13 @@ void emu_fp2_dot2_mont(const uint32_t* in, uint32_t* out0, uint32_t* out1) {
   memcpy(out0, c0.v, 48);
   memcpy(out1, c1.v, 48);
 }
+// [1 - x] R (h2c.hpp clear_cofactor_g1) for a raw affine point R of E(Fp)
+void emu_clear_cofactor(const uint32_t* x, const uint32_t* y, uint32_t* out, int* inf) {
+  g1a r = clear_cofactor_g1(to_mont(load_raw(x)), to_mont(load_raw(y)));
+  *inf = r.inf;
+  store_raw(r.x, out);
+  store_raw(r.y, out + 12);
+}
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
 // safegcd inverse of a Montgomery-domain value in [0, 2p); out canonical Montgomery
 void emu_fp_inv_mont(const uint32_t* a, uint32_t* out) {

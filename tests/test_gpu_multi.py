@@ -262,7 +262,7 @@ def test_var_sharded_single_rank(ctx, comm_ctx, vectors):
 
 
 LONE_RANK = r"""
-import sys, time
+import os, sys, time
 sys.path.insert(0, sys.argv[1])
 from cess_amd import bls
 bls.load_library()
@@ -272,8 +272,10 @@ try:
     c.comm_init(2, 0, bls.comm_id())      # rank 1 never arrives
     print("STATUS 0", time.time() - t0)
 except bls.BlsInfraError as ex:
-    print("STATUS", ex.status, time.time() - t0)
+    print("STATUS", ex.status, time.time() - t0, flush=True)
 c.close()
+print("CLOSED", flush=True)
+os._exit(0)   # RCCL's bootstrap thread stays blocked: end with _exit (include/cess_bls.h)
 """
 
 
@@ -288,7 +290,7 @@ def test_rccl_lone_rank_fails_within_deadline():
     env = dict(os.environ, CESS_BLS_COMM_TIMEOUT_MS="4000", HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run([sys.executable, "-c", LONE_RANK, root], env=env, capture_output=True, text=True, timeout=100)
     line = [x for x in p.stdout.splitlines() if x.startswith("STATUS")]
-    assert p.returncode == 0 and line, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    assert p.returncode == 0 and line and "CLOSED" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
     _, st, dt = line[-1].split()
     assert int(st) == bls.E_COMM, line
     assert 3.5 < float(dt) < 60, line

@@ -97,24 +97,32 @@ class RcclTransport final : public Transport {
     HIPCHK(hipStreamCreateWithFlags(&ctl_, hipStreamNonBlocking));
     // RCCL's bootstrap blocks the calling thread until every rank has
     // connected, even for a non-blocking communicator (measured on MI355X:
-    // ncclCommInitRankConfig never returned for a lone rank), so the call runs
-    // on a helper thread and this one waits for it against the deadline.  A
-    // helper that returns after the caller gave up aborts its communicator
-    // itself; one that never returns stays blocked in the bootstrap (detached:
-    // it holds only the shared job state).
+    // ncclCommInitRankConfig never returned for a lone rank), so the whole
+    // init -- the call and, for the non-blocking communicator, polling its
+    // state to ncclSuccess -- runs on a helper thread (which also owns the
+    // config RCCL may read asynchronously), and this thread waits for it
+    // against the deadline.  A helper that finishes after the caller gave up
+    // aborts its communicator itself; one that never returns stays blocked in
+    // the bootstrap (detached: it holds only the shared job state).
     struct InitJob {
-      std::atomic<int> state{0};   // 0 running, 1 returned, 2 abandoned by the caller
+      std::atomic<int> state{0};   // 0 running, 1 done, 2 abandoned by the caller
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
       ncclComm_t comm = nullptr;
       ncclResult_t res = ncclInternalError;
     };
     auto job = std::make_shared<InitJob>();
+    job->cfg.blocking = 0;
     CTRACE("init rank %d of %d: ncclCommInitRankConfig (non-blocking) on a helper thread", rank, nranks);
     std::thread([job, dev = dev_, nranks, rank, id]() {
       (void)hipSetDevice(dev);
-      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-      cfg.blocking = 0;
       ncclComm_t comm = nullptr;
-      const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &cfg);
+      ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &job->cfg);
+      while (r == ncclInProgress && comm && job->state.load() == 0) {
+        ncclResult_t st = ncclInProgress;
+        if (ncclCommGetAsyncError(comm, &st) != ncclSuccess) st = ncclInternalError;
+        r = st;
+        if (r == ncclInProgress) usleep(200);
+      }
       job->comm = comm;
       job->res = r;
       int running = 0;
@@ -128,18 +136,18 @@ class RcclTransport final : public Transport {
           CTRACE("init: deadline passed with the bootstrap still waiting for peers");
           return CESS_BLS_E_COMM;
         }
-        break;   // it returned just now
+        break;   // it finished just now
       }
       if (spins > 256) usleep(spins > 4096 ? 1000 : 50);
     }
     comm_ = job->comm;
-    CTRACE("init returned %d", (int)job->res);
-    if (job->res != ncclSuccess && job->res != ncclInProgress) {
+    CTRACE("init finished: %d", (int)job->res);
+    if (job->res != ncclSuccess) {
       if (comm_) (void)ncclCommAbort(comm_);
       comm_ = nullptr;
       return CESS_BLS_E_RCCL;
     }
-    return wait_ready();
+    return CESS_BLS_OK;
   }
 
   int allgather_dev(int dev, void* dbuf, size_t bytes, hipStream_t s) override {

@@ -82,6 +82,61 @@ CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink, g2p* t = null
   if (t) *t = r;
 }
 
+// The same iteration with every coefficient handed to emit(k, j, c_j) as soon
+// as it is computed and the key read through q(x, y) where it is needed (a
+// store, e.g. LDS), so fewer Fp2 values are live at the doubling step's peak:
+// k_prepare (two waves per SIMD, 256 VGPRs) spilled 195 VGPRs (940 B/lane of
+// scratch) with the value-returning steps above and the key in registers.
+// Every multiply is sequenced (field.hpp seq), so the program order below is
+// the order the values are produced and die in.
+template <class Emit>
+CESS_HD void doubling_step_emit(g2p& r, int k, Emit&& emit) {
+  emit(k, 1, neg(mul3(sqr(r.x))));                      // -3 X^2
+  const fp2 A2 = mul(r.x, r.y);                         // 2A; X dead
+  const fp2 B = sqr(r.y), C = sqr(r.z);
+  const fp2 H = sub(sub(sqr(add(r.y, r.z)), B), C);     // 2YZ; Y, Z dead
+  emit(k, 0, H);
+  const fp2 E = mul3(mul4(mul_nr(C)));                  // 3 b' Z^2; C dead
+  emit(k, 2, sub(B, E));
+  const fp2 F = mul3(E);
+  const fp2 nx = dbl(mul(A2, sub(B, F)));
+  const fp2 ny = sub(sqr(add(B, F)), mul4(mul3(sqr(E))));
+  r = {nx, ny, mul4(mul(B, H))};
+}
+template <class QL, class Emit>
+CESS_HD void addition_step_emit(g2p& r, QL&& q, int k, Emit&& emit) {
+  fp2 qx, qy;
+  q(qx, qy);
+  const fp2 th = sub(r.y, mul(qy, r.z));
+  const fp2 la = sub(r.x, mul(qx, r.z));
+  emit(k, 0, la);
+  emit(k, 1, neg(th));
+  emit(k, 2, sub(mul(th, qx), mul(la, qy)));
+  const fp2 D = sqr(la);
+  const fp2 E3 = mul(la, D);
+  const fp2 G = mul(r.x, D);
+  const fp2 H = sub(add(E3, mul(r.z, sqr(th))), dbl(G));
+  r = {mul(la, H), sub(mul(th, sub(G, H)), mul(r.y, E3)), mul(r.z, E3)};
+}
+// g2_prepare with emit(k, j, c_j) per coefficient and the key behind q(x, y);
+// returns T = [|x|]Q (by value: an out-pointer to a local puts it in scratch)
+template <class QL, class Emit>
+CESS_HD g2p g2_prepare_emit(QL&& q, Emit&& emit) {
+  g2p r;
+  q(r.x, r.y);
+  r.z = fp2_one();
+  int idx = 0;
+#pragma unroll 1
+  for (int b = 61; b >= 0; b--) {
+    doubling_step_emit(r, idx++, emit);
+    CESS_MEMBAR();
+    if (loop_bit(b)) addition_step_emit(r, q, idx++, emit);
+    CESS_MEMBAR();
+  }
+  doubling_step_emit(r, idx++, emit);
+  return r;
+}
+
 // Scale a line by 1/c2: (c0, c1, c2) -> (c0/c2, c1/c2, 1).  Every Fp2 factor of
 // the Miller-loop value dies in the final exponentiation ((p^2 - 1) divides
 // (p^12 - 1)/r), so the Gt value is unchanged, and the sparse product with a

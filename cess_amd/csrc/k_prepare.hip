@@ -21,16 +21,40 @@ __global__ CESS_LB void k_prepare(uint64_t n, const uint32_t* __restrict__ pk_af
                                   const uint8_t* __restrict__ inf) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  g2p t;
+  // the key (2 Fp2 = 12 uint4 per lane) parked in LDS for the whole
+  // iteration: read at the five addition steps and the subgroup check only
+  // (48 KiB per block, two blocks per CU)
+  __shared__ uint4 QP[12][256];
   {
-    fp2 qx = ld_fp2(pk_aff, stride, i);
-    fp2 qy = ld_fp2(pk_aff + 24 * stride, stride, i);
-    g2_prepare(qx, qy, [&](int k, const coeff3& c) { st_coeff4(coeffs, stride, i, k, c); }, &t);
+    const uint32_t t0 = threadIdx.x;
+    const fp2 qx = ld_fp2(pk_aff, stride, i), qy = ld_fp2(pk_aff + 24 * stride, stride, i);
+#pragma unroll
+    for (int w = 0; w < 6; w++) {
+      const fp& a = w < 3 ? qx.c0 : qx.c1;
+      QP[w][t0] = make_uint4(a.v[4 * (w % 3)], a.v[4 * (w % 3) + 1], a.v[4 * (w % 3) + 2], a.v[4 * (w % 3) + 3]);
+      const fp& b = w < 3 ? qy.c0 : qy.c1;
+      QP[6 + w][t0] = make_uint4(b.v[4 * (w % 3)], b.v[4 * (w % 3) + 1], b.v[4 * (w % 3) + 2], b.v[4 * (w % 3) + 3]);
+    }
   }
+  const uint32_t w0 = wave_first_thread();
+  auto q = [&](fp2& x, fp2& y) {
+    const uint32_t t = w0 + lane_fresh();
+#pragma unroll
+    for (int w = 0; w < 6; w++) {
+      const uint4 a = QP[w][t], b = QP[6 + w][t];
+      fp& da = w < 3 ? x.c0 : x.c1;
+      fp& db = w < 3 ? y.c0 : y.c1;
+      const int o = 4 * (w % 3);
+      da.v[o] = a.x, da.v[o + 1] = a.y, da.v[o + 2] = a.z, da.v[o + 3] = a.w;
+      db.v[o] = b.x, db.v[o + 1] = b.y, db.v[o + 2] = b.z, db.v[o + 3] = b.w;
+    }
+  };
+  const g2p t = g2_prepare_emit(q, [&](int k, int j, const fp2& c) { st_coeff4_one(coeffs, stride, i, k, j, c); });
   if (code && code[i] == 0 && !(inf[i] & INF_PK)) {
     CESS_MEMBAR();
-    if (!g2_psi_is_neg_proj(ld_fp2(pk_aff, stride, i), ld_fp2(pk_aff + 24 * stride, stride, i), t.x, t.y, t.z))
-      code[i] = CODE_PK_POINT;
+    fp2 qx, qy;
+    q(qx, qy);
+    if (!g2_psi_is_neg_proj(qx, qy, t.x, t.y, t.z)) code[i] = CODE_PK_POINT;
   }
 }
 

@@ -57,6 +57,13 @@ CESS_HD void st_coeff4(uint4* __restrict__ base, uint64_t stride, uint32_t i, in
   for (int q = 0; q < 18; q++)
     base[(uint64_t)(18 * k + q) * stride + i] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
+// one coefficient (j = 0, 1, 2: c0, c1, c2) of line k, rows 18k + 6j .. +5
+CESS_HD void st_coeff4_one(uint4* __restrict__ base, uint64_t stride, uint32_t i, int k, int j, const fp2& c) {
+  const uint32_t* w = &c.c0.v[0];
+#pragma unroll
+  for (int q = 0; q < 6; q++)
+    base[(uint64_t)(18 * k + 6 * j + q) * stride + i] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
 // wave-uniform coefficient table (the -G2 constant): stride 1, same address in every lane
 CESS_HD coeff3 ld_coeff_uniform(const uint32_t* tab, int k) {
   const uint32_t* b = tab + 72 * k;

@@ -216,8 +216,18 @@ int emu_g2_accept(const uint8_t* pk, int split) {
   if (!split) return g2_decompress(wp, q) ? (q.inf ? 2 : 1) : 0;
   if (!g2_decompress(wp, q, RegPark2{}, false)) return 0;
   if (q.inf) return 2;
-  g2p t;
-  g2_prepare(q.x, q.y, [](int, const coeff3&) {}, &t);
+  // the kernel's form (pairing.hpp g2_prepare_emit, key behind a loader),
+  // checked coefficient by coefficient against the value-returning iteration
+  static coeff3 ref[N_COEFFS];
+  g2p t0;
+  g2_prepare(q.x, q.y, [](int k, const coeff3& c) { ref[k] = c; }, &t0);
+  bool same = true;
+  const g2p t = g2_prepare_emit([&](fp2& x, fp2& y) { x = q.x, y = q.y; },
+                                [&](int k, int j, const fp2& c) {
+                                  const fp2& r = j == 0 ? ref[k].c0 : j == 1 ? ref[k].c1 : ref[k].c2;
+                                  same = same && eq(r, c);
+                                });
+  if (!same || !eq(t.x, t0.x) || !eq(t.y, t0.y) || !eq(t.z, t0.z)) return -1;
   return g2_psi_is_neg_proj(q.x, q.y, t.x, t.y, t.z) ? 1 : 0;
 }
 

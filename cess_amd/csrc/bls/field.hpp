@@ -405,8 +405,10 @@ CESS_HD fp from_mont(const fp& a) {
 }
 CESS_HD fp to_mont(const fp& a_raw) { return mul(a_raw, fp_from(c::R2)); }
 
-// a^e for a fixed 12-word exponent: MSB-first sliding window of width 3 over
-// the odd powers a, a^3, a^5, a^7 (table held in registers; the window is
+// a^e for a fixed 12-word exponent: MSB-first sliding window of width W
+// (CESS_POW_W, default 4: decode/hash kernels 1-3 % faster than width 3 on
+// one MI355X, width 5 spills -- profiles/round4_d_sweep.txt) over the odd
+// powers a, a^3, .., a^(2^W - 1) (table held in registers; the window is
 // picked with uniform selects, not a dynamically indexed array, so nothing goes
 // to scratch).  For the 379-381-bit exponents used here (p-2, (p+1)/4,
 // (p-3)/4; ~229 set bits) this is ~110 multiplies instead of ~229.  All
@@ -460,17 +462,20 @@ CESS_HD void sqr_d(uint32_t (&x)[14]) {
   seq14(x);
 }
 CESS_HD uint32_t exp_bit(const uint32_t (&e)[12], int i) { return (e[i >> 5] >> (i & 31)) & 1u; }
+#ifndef CESS_POW_W
+#define CESS_POW_W 4
+#endif
 CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
+  constexpr int W = CESS_POW_W, NT = 1 << (W - 1);   // odd powers a, a^3, .., a^(2^W - 1)
   fp a = a0;
   seq(a);
-  uint32_t t1[14], t3[14], t5[14], t7[14], a2[14], r[14], w[14];
-  unpack28(a, t1);
+  uint32_t t[NT][14], a2[14], r[14], w[14];
+  unpack28(a, t[0]);
 #pragma unroll
-  for (int q = 0; q < 14; q++) a2[q] = t1[q];
+  for (int q = 0; q < 14; q++) a2[q] = t[0][q];
   sqr_d(a2);
-  mul_d(t3, t1, a2);
-  mul_d(t5, t3, a2);
-  mul_d(t7, t5, a2);
+#pragma unroll
+  for (int j = 1; j < NT; j++) mul_d(t[j], t[j - 1], a2);
   bool started = false;
   int i = 383;
 #pragma unroll 1
@@ -480,7 +485,7 @@ CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
       i--;
       continue;
     }
-    int j = i >= 2 ? i - 2 : 0;   // window e[i..j], j the lowest set bit in it
+    int j = i >= W - 1 ? i - (W - 1) : 0;   // window e[i..j], j the lowest set bit in it
     while (!exp_bit(e, j)) j++;
     uint32_t v = 0;
 #pragma unroll 1
@@ -488,8 +493,14 @@ CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
       v = 2 * v + exp_bit(e, k);
       if (started) sqr_d(r);
     }
+    // uniform selects (v is wave-uniform): no dynamically indexed table
 #pragma unroll
-    for (int q = 0; q < 14; q++) w[q] = v == 1 ? t1[q] : v == 3 ? t3[q] : v == 5 ? t5[q] : t7[q];
+    for (int q = 0; q < 14; q++) {
+      uint32_t x = t[0][q];
+#pragma unroll
+      for (int m = 1; m < NT; m++) x = v == (uint32_t)(2 * m + 1) ? t[m][q] : x;
+      w[q] = x;
+    }
     if (started) {
       mul_d(r, r, w);
     } else {

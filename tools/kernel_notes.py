@@ -10,7 +10,7 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "cess_amd", "lib", "libcess_bls.so")
+LIB = os.environ.get("CESS_BLS_LIB") or os.path.join(ROOT, "cess_amd", "lib", "libcess_bls.so")
 BIN = "/opt/rocm/lib/llvm/bin"
 KEYS = (".vgpr_count", ".agpr_count", ".vgpr_spill_count", ".private_segment_fixed_size", ".group_segment_fixed_size")
 

@@ -754,6 +754,24 @@ CESS_HD fp2 add_nr(const fp2& a, const fp2& b) {
   return r;
 }
 CESS_HD fp2 dbl(const fp2& a) { return {dbl(a.c0), dbl(a.c1)}; }
+// a + xi b unreduced, xi = 1 + u: (a0 + b0 + (2p - b1), a1 + b0 + b1), each
+// component < 6p < 2^384 for a, b < 2p -- for mul() operands only (see
+// add_nr).  Four interleaved carry chains and no conditional subtraction,
+// against mul_nr's two reduced chains plus add_nr.
+CESS_HD fp2 add_xi_nr(const fp2& a, const fp2& b) {
+  fp2 r;
+  uint32_t bn = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t nb1 = subc32(c::P2_RAW[i], b.c1.v[i], bn, &bn);
+    const uint32_t s0 = addc32(a.c0.v[i], b.c0.v[i], k0, &k0);
+    const uint32_t s1 = addc32(a.c1.v[i], b.c0.v[i], k1, &k1);
+    r.c0.v[i] = addc32(s0, nb1, k2, &k2);
+    r.c1.v[i] = addc32(s1, b.c1.v[i], k3, &k3);
+  }
+  return r;
+}
+
 CESS_HD fp2 neg(const fp2& a) { return {neg(a.c0), neg(a.c1)}; }
 CESS_HD fp2 conj(const fp2& a) { return {a.c0, neg(a.c1)}; }
 CESS_HD bool is_zero(const fp2& a) { return is_zero(a.c0) && is_zero(a.c1); }

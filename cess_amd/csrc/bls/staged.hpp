@@ -366,6 +366,37 @@ CESS_HD void inv12(const S& f) {
   st6(f, 1, neg(mul(a1, t)));
 }
 
+// d <- f^-1 with every Fp6 operand streamed (FE_INV): d distinct from f, t a
+// 3-Fp2 temporary store (the LDS park).  f = a0 + a1 w: t = a0^2 - v a1^2,
+// t^-1 = (c0, c1, c2) / (t0 c0 + xi (t2 c1 + t1 c2)) with c0 = t0^2 - xi t1 t2,
+// c1 = xi t2^2 - t0 t1, c2 = t1^2 - t0 t2, then d = (a0 t^-1, -a1 t^-1).  The
+// value-based inv12 above keeps a0, a1 and the squares' temporaries live at
+// once: k_final's largest spill region (575 of its 653 scratch accesses).
+template <class D, class S, class T>
+CESS_HD void inv12_stream(const D& d, const S& f, const T& t) {
+  mul6_stream([&](int j) { return f.ld(j); }, [&](int j) { return f.ld(j); }, [&](int j, const fp2& v) { d.st(j, v); });
+  mul6_stream([&](int j) { return f.ld(3 + j); }, [&](int j) { return f.ld(3 + j); },
+              [&](int j, const fp2& v) { d.st(3 + j, v); });
+  t.st(0, sub(d.ld(0), mul_nr(d.ld(5))));   // a0^2 - v a1^2, v (x0, x1, x2) = (xi x2, x0, x1)
+  t.st(1, sub(d.ld(1), d.ld(3)));
+  t.st(2, sub(d.ld(2), d.ld(4)));
+  CESS_MEMBAR();
+  d.st(0, sub(sqr(t.ld(0)), mul_nr(mul(t.ld(1), t.ld(2)))));
+  CESS_MEMBAR();
+  d.st(1, sub(mul_nr(sqr(t.ld(2))), mul(t.ld(0), t.ld(1))));
+  CESS_MEMBAR();
+  d.st(2, sub(sqr(t.ld(1)), mul(t.ld(0), t.ld(2))));
+  CESS_MEMBAR();
+  const fp2 den = inv(add(mul(t.ld(0), d.ld(0)), mul_nr(add(mul(t.ld(2), d.ld(1)), mul(t.ld(1), d.ld(2))))));
+  CESS_MEMBAR();
+#pragma unroll 1
+  for (int j = 0; j < 3; j++) t.st(j, mul(d.ld(j), den));
+  CESS_MEMBAR();
+  mul6_stream([&](int j) { return f.ld(j); }, [&](int j) { return t.ld(j); }, [&](int j, const fp2& v) { d.st(j, v); });
+  mul6_stream([&](int j) { return f.ld(3 + j); }, [&](int j) { return t.ld(j); },
+              [&](int j, const fp2& v) { d.st(3 + j, neg(v)); });
+}
+
 // ---------------------------------------------------------------------------
 // Final exponentiation as a program over one in-place accumulator A and HBM
 // slots (MillerLoopResult::final_exponentiation, A13).  Each opcode body exists
@@ -474,7 +505,8 @@ CESS_HD void cyc_square_run(const A& acc, const P& pk, int n) {
 // Fp2 squarings.  The factor 3 of both products of a half rides in the digits
 // of one operand (mul_scaled<3>), so b3 = 3 z4 z5 and t3 = 3 (z4 + z5)(z4 + xi
 // z5) give 3 (z4^2 + xi z5^2) = t3 - b3 - xi b3 and 6 xi z4 z5 = 2 xi b3 with
-// four Fp2 additions instead of seven.  z2, z3 stay in registers, z4, z5 in
+// four Fp2 additions instead of seven; z4 + xi z5 is formed unreduced
+// (add_xi_nr, < 6p: 3 (4p)(6p) < p R).  z2, z3 stay in registers, z4, z5 in
 // the parking store `pk` (LDS in k_final, indices 0, 1), and the (z4, z5)
 // half's two results stay in registers while the (z2, z3) half runs: the run
 // touches no HBM (k_final 171.3 -> 160.8 ms per 1 M against z4, z5 in the HBM
@@ -488,7 +520,7 @@ CESS_HD void kcyc_run(const P& pk, fp2& z2, fp2& z3, int n) {
     {
       const fp2 b3 = mul_scaled<3>(pk.ld(0), pk.ld(1));
       CESS_MEMBAR();
-      const fp2 t3 = mul_scaled<3>(add_nr(pk.ld(0), pk.ld(1)), add_nr(pk.ld(0), mul_nr(pk.ld(1))));
+      const fp2 t3 = mul_scaled<3>(add_nr(pk.ld(0), pk.ld(1)), add_xi_nr(pk.ld(0), pk.ld(1)));
       const fp2 nb3 = mul_nr(b3);
       u = sub(sub(t3, b3), nb3);   // 3 (z4^2 + xi z5^2)
       v = dbl(nb3);                // 6 xi z4 z5
@@ -497,7 +529,7 @@ CESS_HD void kcyc_run(const P& pk, fp2& z2, fp2& z3, int n) {
     {
       const fp2 b3 = mul_scaled<3>(z2, z3);
       CESS_MEMBAR();
-      const fp2 t3 = mul_scaled<3>(add_nr(z2, z3), add_nr(z2, mul_nr(z3)));
+      const fp2 t3 = mul_scaled<3>(add_nr(z2, z3), add_xi_nr(z2, z3));
       pk.st(0, sub(sub(sub(t3, b3), mul_nr(b3)), dbl(pk.ld(0))));
       pk.st(1, dbl(add(pk.ld(1), b3)));
     }
@@ -620,7 +652,10 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
       case FE_SQN: cyc_square_run(acc, pk, arg); break;
       case FE_CONJ: conj12(acc); break;
       case FE_FROB: frob12(acc, arg); break;
-      case FE_INV: inv12(acc); break;
+      case FE_INV:   // into the other accumulator, like FE_MUL
+        inv12_stream(cur ? acc0 : acc1, acc, pk);
+        cur ^= 1;
+        break;
       case FE_CHAIN: cyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }, pk); break;
       default: break;
     }

@@ -13,29 +13,7 @@ using namespace cess;
 // alternative placements measured in round 1 (accumulator in HBM, split
 // LDS/HBM, HBM ping-pong with streamed operands: 314 / 244 / 203 vs 191 ms
 // per 1 M) were removed from the product source.
-#ifndef CESS_MILLER_HYBRID
-#define CESS_MILLER_HYBRID 0
-#endif
-#if CESS_MILLER_HYBRID
-// EXPERIMENT (round 4): two waves per SIMD with the accumulator's c0 half in
-// a 72 KiB LDS image and its c1 half in place in the HBM output rows
-#define CESS_LB_F12 __launch_bounds__(256, 2)
-struct HybF12 {
-  LdsF12 lo;
-  GlobF12W hi;
-  CESS_HD fp2 ld(int k) const { return k < 3 ? lo.ld(k) : hi.ld(k); }
-  CESS_HD void st(int k, const fp2& a) const {
-    if (k < 3) lo.st(k, a);
-    else hi.st(k, a);
-  }
-};
-#elif defined(CESS_MILLER_REG256)
-// EXPERIMENT (round 4): the LDS-image loop held to 256 registers, so a wave of
-// another kernel can share each SIMD with k_miller's single wave
-#define CESS_LB_F12 __launch_bounds__(256, 1) __attribute__((amdgpu_num_vgpr(CESS_MILLER_REG256)))
-#else
 #define CESS_LB_F12 __launch_bounds__(256, 1)
-#endif
 
 __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ code,
                                      const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
@@ -51,14 +29,8 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   // batch, its key's row in the distinct-key table (cstride = table stride)
   const uint32_t cj = cidx ? cidx[i] : i;
   uint8_t fl = inf[i];
-#if CESS_MILLER_HYBRID
-  __shared__ uint4 F[18][256];
-  const uint32_t wf = wave_first_thread();
-  HybF12 f{LdsF12{F, wf}, GlobF12W{fout + (uint64_t)blockIdx.x * blockDim.x + wf, stride}};
-#else
   __shared__ uint4 F[36][256];
   LdsF12 f{F, wave_first_thread()};
-#endif
   // the G1 points are re-read from L2 for every line: held in 48 registers
   // across the loop they cost 27 spilled VGPRs (112 B/lane of scratch) and
   // +0.4 ms (profiles/round3_z_sweep.txt; round 2: 163 -> 171 ms)
@@ -90,10 +62,5 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   // costs 22 ms per 1 M against 18 ms saved here, profiles/round3_k_sweep.txt.)
   const bool norm1 = cnorm && cnorm[cj];
   miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1);
-#if CESS_MILLER_HYBRID
-#pragma unroll 1
-  for (int k = 0; k < 3; k++) f.hi.st(k, f.lo.ld(k));   // c1 is already in place
-#else
   copy12(GlobF12{fout, stride, i}, f);
-#endif
 }

@@ -431,9 +431,6 @@ def run_rsa(args, ctx, rank, world):
             "config": {"workload": f"SURVEY §8(f) rank 4, cp_enclave_verify::verify_rsa: {n} sigs per GPU, inputs in HBM",
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
-            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
-            "host_buffers": host_rate,
-            "comm": comm,
             "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
             "roofline": {"bound": "valu-int", "kernel": "k_rsa_verify_2048u",
                          "achieved": achieved / 1e12, "peak": PEAK_MADS / 1e12,
@@ -522,9 +519,6 @@ def run_sign(args, ctx, rank, world):
             "config": {"workload": f"SURVEY §8(f) rank 3, batch PrivateKey::sign: {n} records per GPU",
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
-            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
-            "host_buffers": host_rate,
-            "comm": comm,
             "stage_ms_per_step": {k: v[0] / args.steps for k, v in st.items()},
             "roofline": {"bound": "valu-int", "kernel": "k_sign", "achieved": achieved / 1e12,
                          "peak": PEAK_MADS / 1e12, "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
@@ -626,9 +620,7 @@ def run_rlc(args, ctx, rank, world):
                                    f"{args.forged_count} forged per GPU, RLC + Gt-partial RCCL all-gather + bisection",
                        "timing": "host-buffer API incl. key dedup and PCIe", "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
-            "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
-            "host_buffers": host_rate,
-            "comm": comm, "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
+            "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
             "runtime": runtime_provenance(),
         }), flush=True)
 

@@ -313,17 +313,19 @@ extern "C" int cess_bls_comm_info(cess_bls_ctx* c, int* nranks_out, int* rank_ou
   ENTRY(c);
   if (!c->xport) return CESS_BLS_E_NO_COMM;
   int nr = 0, rk = 0;
-  int r = c->xport->comm_count(&nr, &rk);
-  if (r) return r;
-  if (nranks_out) *nranks_out = nr;
-  if (rank_out) *rank_out = rk;
-  if (!bus_ids_out) return CESS_BLS_OK;
-  // collective: every rank's PCI bus id, gathered in rank order
+  int st = c->xport->comm_count(&nr, &rk);
+  if (!st) {
+    if (nranks_out) *nranks_out = nr;
+    if (rank_out) *rank_out = rk;
+  }
+  if (!bus_ids_out) return st;
+  // collective: every rank's PCI bus id, gathered in rank order; a local
+  // failure (count or bus id) still joins the agreement, so no peer is left
+  // waiting in it
   std::vector<char> ids((size_t)c->nranks * CESS_BLS_BUS_ID_BYTES, 0);
   char* mine = &ids[(size_t)c->rank * CESS_BLS_BUS_ID_BYTES];
-  const int st = hipDeviceGetPCIBusId(mine, CESS_BLS_BUS_ID_BYTES - 1, c->device) == hipSuccess ? CESS_BLS_OK
-                                                                                                 : CESS_BLS_E_HIP;
-  r = agree(*c->xport, st);
+  if (!st && hipDeviceGetPCIBusId(mine, CESS_BLS_BUS_ID_BYTES - 1, c->device) != hipSuccess) st = CESS_BLS_E_HIP;
+  int r = agree(*c->xport, st);
   if (r) return r;
   r = c->xport->allgather_host(ids.data(), CESS_BLS_BUS_ID_BYTES);
   if (r) return r;

@@ -43,6 +43,17 @@ __global__ void k_g1_sum_segs(uint32_t, const uint64_t*, const uint64_t*, const 
 __global__ void k_rlc_pairs_list(uint32_t, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint8_t*, uint8_t*,
                                  uint8_t*, uint32_t*, uint32_t*, const uint32_t*);
 __global__ void k_fp12_prod_segs(uint32_t, const uint32_t*, const uint4*, uint64_t, uint4*, uint4*);
+__global__ void k_msm_count(uint64_t, const uint8_t*, const uint8_t*, MsmSegs, const uint32_t*, uint64_t, uint32_t*);
+__global__ void k_msm_scatter(uint64_t, const uint8_t*, const uint8_t*, MsmSegs, const uint32_t*, uint64_t, uint32_t*,
+                              uint32_t*);
+__global__ void k_inv_perm(uint64_t, const uint32_t*, uint32_t*);
+__global__ void k_msm_aos(uint64_t, const uint32_t*, uint4*);
+__global__ void k_msm_items(uint32_t, uint32_t, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                            const uint4*, const uint4*, uint32_t*, uint64_t);
+__global__ void k_msm_bucket_sum(uint32_t, const uint32_t*, const uint32_t*, uint64_t, uint32_t*);
+__global__ void k_msm_window(uint32_t, const uint32_t*, uint64_t, uint32_t*);
+__global__ void k_msm_wsum(uint32_t, const uint32_t*, uint32_t*);
+__global__ void k_msm_finish(uint32_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*);
 
 namespace cess_host {
 
@@ -95,6 +106,13 @@ struct RlcState {
   DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
   DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, rec_f2, acc, slots, fin_code, fin_bm, gt, gts, tmp;
   DevBuf seg, part2, rec_coeffs, lists, d_gt_all;
+  // bucket sums of the first check (k_msm_*): records' affine points and codes
+  // for the whole batch (SoA stride n), group ids, bucket tables
+  bool pts = false;                 // the batch's points are kept on the device (bucket sums possible)
+  bool pq = false;                  // P, Q (per-record multiples) computed
+  bool aos = false, have_pos = false;
+  uint64_t index_hi = 0;            // scalar index base of this batch (rlc_begin_at)
+  DevBuf Xs, Xh, Xsa, Xha, d_pos, m_bounds, d_code, d_inf, d_grp, m_cnt, m_start, m_cur, m_items, m_idx, m_part, m_bsum, m_T, m_U;
 };
 
 // Stage buffers of one in-flight pipeline part (SoA, stride = qcap).

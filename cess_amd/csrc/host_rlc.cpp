@@ -5,6 +5,8 @@
 // cess_bls_verify_batch (up to the 2^-127 soundness error per check).
 #include <sys/random.h>
 
+#include <thread>
+
 #include "host.hpp"
 
 using namespace cess_host;
@@ -56,11 +58,196 @@ static int rlc_sums(RlcState& R, hipStream_t s, const std::vector<uint64_t>& off
   return CESS_BLS_OK;
 }
 
+// Open-addressing table of distinct 96-byte keys (ids in insertion order).
+struct KeyTable {
+  const uint8_t* pks;
+  std::vector<uint64_t> first;       // record index of each id's first occurrence
+  std::vector<uint32_t> slot = std::vector<uint32_t>(64, 0);   // id + 1; 0 = empty
+  uint64_t mask = 63;
+  static uint64_t khash(const uint8_t* k) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int q = 0; q < 96; q += 8) {
+      uint64_t w;
+      memcpy(&w, k + q, 8);
+      h = (h ^ w) * 0xff51afd7ed558ccdull;
+      h ^= h >> 29;
+    }
+    return h;
+  }
+  // id of record i's key, inserting it (first occurrence i) if new
+  uint32_t id(uint64_t i) {
+    const uint8_t* k = pks + 96 * i;
+    uint64_t h = khash(k) & mask;
+    while (slot[h] && memcmp(pks + 96 * first[slot[h] - 1], k, 96) != 0) h = (h + 1) & mask;
+    if (slot[h]) return slot[h] - 1;
+    first.push_back(i);
+    slot[h] = (uint32_t)first.size();
+    if (2 * first.size() > mask) {   // grow and rehash
+      std::vector<uint32_t> ns(2 * (mask + 1), 0);
+      const uint64_t nm = 2 * (mask + 1) - 1;
+      for (uint32_t g = 0; g < first.size(); g++) {
+        uint64_t q = khash(pks + 96 * first[g]) & nm;
+        while (ns[q]) q = (q + 1) & nm;
+        ns[q] = g + 1;
+      }
+      slot.swap(ns);
+      mask = nm;
+    }
+    return (uint32_t)first.size() - 1;
+  }
+};
+
+// grp[i] = group of record i's key, groups numbered by first occurrence;
+// first[g] = that record.  Up to 16 host threads over contiguous slices.
+static void group_keys(const uint8_t* pks, uint64_t n, std::vector<uint32_t>& grp, std::vector<uint64_t>& first) {
+  const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>(16, n / 65536));
+  std::vector<KeyTable> loc(T, KeyTable{pks});
+  std::vector<std::thread> th;
+  auto run = [&](uint64_t t) {
+    for (uint64_t i = n * t / T; i < n * (t + 1) / T; i++) grp[i] = loc[t].id(i);
+  };
+  for (uint64_t t = 1; t < T; t++) th.emplace_back(run, t);
+  run(0);
+  for (auto& x : th) x.join();
+  KeyTable glob{pks};
+  std::vector<std::vector<uint32_t>> remap(T);
+  for (uint64_t t = 0; t < T; t++)
+    for (uint64_t f : loc[t].first) remap[t].push_back(glob.id(f));
+  first.swap(glob.first);
+  if (T == 1) return;   // one slice: its ids are the global ids already
+  th.clear();
+  auto rm = [&](uint64_t t) {
+    for (uint64_t i = n * t / T; i < n * (t + 1) / T; i++) grp[i] = remap[t][grp[i]];
+  };
+  for (uint64_t t = 1; t < T; t++) th.emplace_back(rm, t);
+  rm(0);
+  for (auto& x : th) x.join();
+}
+
+// Bucket sums (k_rlc.hip, k_msm_*).  env CESS_BLS_RLC_MSM = 0: never (each
+// record's multiples P_i, Q_i as before), 1: for every check whose segment
+// count fits the tables; default: also at least 64 covered records per
+// segment (a segment costs ~4,096 bucket combinations, a record ~32 additions
+// against one 128-bit multiple per point).
+static int msm_env() {
+  const char* e = getenv("CESS_BLS_RLC_MSM");
+  return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 1 : 2;
+}
+static bool msm_ok(uint64_t covered, uint64_t segs) {
+  const int e = msm_env();
+  if (e == 0 || segs == 0 || segs > CESS_MSM_MAX_SEGS || 32 * covered >= (1ull << 32)) return false;
+  return e == 1 || covered >= 64 * segs;
+}
+
+// Sums of one check from the batch's points: S[q] = sum_{i in part q} r_i sig_i
+// (stride NR), Qs[t] = sum_{i in term t} r_i H_i (stride M), over the records
+// with code 0 (identity terms excluded).  Count entries per bucket, lay the
+// buckets out (host prefix sums over the counts), scatter the record ids, sum
+// each bucket in chunks and the chunks per bucket, then the window running
+// sums and the 2^(8w) weights.
+static int msm_sums(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& parts,
+                    const std::vector<Term>& terms, uint32_t* S, uint32_t* Qs) {
+  hipStream_t s = c->stream;
+  const uint64_t n = R.n, NR = parts.size(), M = terms.size(), nseg = NR + M, nb = nseg * CESS_MSM_SEG_BUCKETS;
+  const uint32_t* seed = R.d_seed.as<uint32_t>();
+  // the batch's first check: one part = the batch, term g = group g
+  bool first = NR == 1 && parts[0].first == 0 && parts[0].second == n && M == R.K;
+  for (uint64_t t = 0; first && t < M; t++) first = terms[t].group == t;
+  MsmSegs sg{R.d_grp.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)NR, (uint32_t)M};
+  int r = R.m_cnt.ensure(nb * 4) | R.m_start.ensure(nb * 4) | R.m_cur.ensure(nb * 4) | R.m_items.ensure((nb + 1) * 4);
+  r |= R.m_bsum.ensure(nb * 36 * 4) | R.m_T.ensure(nseg * 256 * 36 * 4) | R.m_U.ensure(nseg * 16 * 36 * 4);
+  r |= R.m_bounds.ensure(2 * nseg * 4);
+  if (!first) r |= R.d_pos.ensure(n * 4);
+  if (r) return CESS_BLS_E_OOM;
+  std::vector<uint32_t> bounds(2 * nseg);
+  if (!first) {
+    if (!R.have_pos) {
+      hipLaunchKernelGGL(k_inv_perm, dim3(grid_for(n)), dim3(kBlock), 0, s, n, (const uint32_t*)R.d_perm.as<uint32_t>(),
+                         R.d_pos.as<uint32_t>());
+      R.have_pos = true;
+    }
+    for (uint64_t q = 0; q < NR; q++) bounds[q] = (uint32_t)parts[q].first, bounds[NR + q] = (uint32_t)parts[q].second;
+    for (uint64_t t = 0; t < M; t++)
+      bounds[2 * NR + t] = (uint32_t)terms[t].lo, bounds[2 * NR + M + t] = (uint32_t)terms[t].hi;
+    HIPCHK(hipMemcpyAsync(R.m_bounds.p, bounds.data(), bounds.size() * 4, hipMemcpyHostToDevice, s));
+    const uint32_t* d = R.m_bounds.as<uint32_t>();
+    sg = {nullptr, R.d_pos.as<uint32_t>(), d, d + NR, d + 2 * NR, d + 2 * NR + M, (uint32_t)NR, (uint32_t)M};
+  }
+  HIPCHK(hipMemsetAsync(R.m_cnt.p, 0, nb * 4, s));
+  hipLaunchKernelGGL(k_msm_count, dim3(grid_for(n)), dim3(kBlock), 0, s, n, (const uint8_t*)R.d_code.as<uint8_t>(),
+                     (const uint8_t*)R.d_inf.as<uint8_t>(), sg, seed, R.index_hi, R.m_cnt.as<uint32_t>());
+  HIPCHK(hipGetLastError());
+  std::vector<uint32_t> cnt(nb), start(nb), items(nb + 1);
+  HIPCHK(hipMemcpyAsync(cnt.data(), R.m_cnt.p, nb * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  uint64_t e = 0, it = 0;
+  for (uint64_t b = 0; b < nb; b++) {
+    start[b] = (uint32_t)e;
+    items[b] = (uint32_t)it;
+    e += cnt[b];
+    if (cnt[b]) it += (cnt[b] + msm_chunk(cnt[b]) - 1) / msm_chunk(cnt[b]);
+  }
+  items[nb] = (uint32_t)it;
+  if (e >= (1ull << 32) || it >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
+  if (R.m_idx.ensure(std::max<uint64_t>(e, 1) * 4) || R.m_part.ensure(std::max<uint64_t>(it, 1) * 36 * 4))
+    return CESS_BLS_E_OOM;
+  HIPCHK(hipMemcpyAsync(R.m_start.p, start.data(), nb * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(R.m_cur.p, start.data(), nb * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(R.m_items.p, items.data(), (nb + 1) * 4, hipMemcpyHostToDevice, s));
+  if (e) {
+    if (!R.aos) {   // the points record-major, once per batch
+      if (R.Xsa.ensure(n * 96) || R.Xha.ensure(n * 96)) return CESS_BLS_E_OOM;
+      hipLaunchKernelGGL(k_msm_aos, dim3(grid_for(n)), dim3(kBlock), 0, s, n, (const uint32_t*)R.Xs.as<uint32_t>(),
+                         R.Xsa.as<uint4>());
+      hipLaunchKernelGGL(k_msm_aos, dim3(grid_for(n)), dim3(kBlock), 0, s, n, (const uint32_t*)R.Xh.as<uint32_t>(),
+                         R.Xha.as<uint4>());
+      R.aos = true;
+    }
+    hipLaunchKernelGGL(k_msm_scatter, dim3(grid_for(n)), dim3(kBlock), 0, s, n, (const uint8_t*)R.d_code.as<uint8_t>(),
+                       (const uint8_t*)R.d_inf.as<uint8_t>(), sg, seed, R.index_hi, R.m_cur.as<uint32_t>(),
+                       R.m_idx.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_items, dim3(grid_for(it)), dim3(kBlock), 0, s, (uint32_t)it, (uint32_t)nb, (uint32_t)NR,
+                       (const uint32_t*)R.m_items.as<uint32_t>(), (const uint32_t*)R.m_start.as<uint32_t>(),
+                       (const uint32_t*)R.m_cnt.as<uint32_t>(), (const uint32_t*)R.m_idx.as<uint32_t>(),
+                       (const uint4*)R.Xsa.as<uint4>(), (const uint4*)R.Xha.as<uint4>(), R.m_part.as<uint32_t>(), it);
+  }
+  hipLaunchKernelGGL(k_msm_bucket_sum, dim3(grid_for(nb)), dim3(kBlock), 0, s, (uint32_t)nb,
+                     (const uint32_t*)R.m_items.as<uint32_t>(), (const uint32_t*)R.m_part.as<uint32_t>(),
+                     std::max<uint64_t>(it, 1), R.m_bsum.as<uint32_t>());
+  hipLaunchKernelGGL(k_msm_window, dim3(grid_for(nseg * 256)), dim3(kBlock), 0, s, (uint32_t)nseg,
+                     (const uint32_t*)R.m_bsum.as<uint32_t>(), nb, R.m_T.as<uint32_t>());
+  hipLaunchKernelGGL(k_msm_wsum, dim3(grid_for(nseg * 16)), dim3(kBlock), 0, s, (uint32_t)nseg,
+                     (const uint32_t*)R.m_T.as<uint32_t>(), R.m_U.as<uint32_t>());
+  hipLaunchKernelGGL(k_msm_finish, dim3(grid_for(nseg)), dim3(kBlock), 0, s, (uint32_t)nseg, (uint32_t)NR,
+                     (const uint32_t*)R.m_U.as<uint32_t>(), S, Qs);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));   // bounds / start / items are host vectors
+  return CESS_BLS_OK;
+}
+
+// the per-record multiples P_i = r_i sig_i, Q_i = r_i H_i (a check with too
+// many segments for the buckets sums them over its ranges), once per batch
+static int rlc_scale_all(cess_bls_ctx* c, RlcState& R) {
+  if (R.pq) return CESS_BLS_OK;
+  hipStream_t s = c->stream;
+  if (R.P.ensure(R.n * 36 * 4) | R.Q.ensure(R.n * 36 * 4)) return CESS_BLS_E_OOM;
+  hipLaunchKernelGGL(k_rlc_scale, dim3(grid_for(R.n)), dim3(kBlock), 0, s, R.n, (const uint8_t*)R.d_code.as<uint8_t>(),
+                     (const uint8_t*)R.d_inf.as<uint8_t>(), (const uint32_t*)R.Xs.as<uint32_t>(),
+                     (const uint32_t*)R.Xh.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(), R.index_hi,
+                     R.P.as<uint32_t>(), R.Q.as<uint32_t>(), R.n, R.n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  R.pq = true;
+  return CESS_BLS_OK;
+}
+
 // RLC checks of NR perm-position ranges in one batch: ok[r] = the product of
 // range r's pairings is 1.  Only the (range, key group) terms that intersect
 // are formed (perm is sorted by group, so a range meets a contiguous run of
 // groups): at most NR + K + NR terms per batch, never NR * K.  gt_out
-// (optional, NR == 1): the Gt value of the check.
+// (optional, NR == 1): the Gt value of the check.  The sums come from the
+// buckets (msm_sums) when the batch's points are on the device and msm_ok,
+// else from the per-record multiples.
 static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
                            std::vector<uint8_t>& ok, uint8_t* gt_out) {
   hipStream_t s = c->stream;
@@ -113,10 +300,19 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
   const uint32_t* d_range = R.lists.as<uint32_t>();
   const uint32_t* d_group = d_range + M;
   const uint32_t* d_tbeg = d_range + 2 * M;
-  r = rlc_sums(R, s, so, sc, R.P.as<uint32_t>(), R.n, R.S.as<uint32_t>(), NR);
-  if (r) return r;
-  r = rlc_sums(R, s, qo, qc, R.Q.as<uint32_t>(), R.n, R.Qs.as<uint32_t>(), M);
-  if (r) return r;
+  uint64_t covered = 0;
+  for (uint64_t q = 0; q < NR; q++) covered += sc[q];
+  if (R.pts && msm_ok(covered, NR + M)) {
+    r = msm_sums(c, R, rg, terms, R.S.as<uint32_t>(), R.Qs.as<uint32_t>());
+    if (r) return r;
+  } else {
+    r = rlc_scale_all(c, R);
+    if (r) return r;
+    r = rlc_sums(R, s, so, sc, R.P.as<uint32_t>(), R.n, R.S.as<uint32_t>(), NR);
+    if (r) return r;
+    r = rlc_sums(R, s, qo, qc, R.Q.as<uint32_t>(), R.n, R.Qs.as<uint32_t>(), M);
+    if (r) return r;
+  }
   hipLaunchKernelGGL(k_rlc_pairs_list, dim3((unsigned)((M + 63) / 64)), dim3(64), 0, s, (uint32_t)M, (uint32_t)NR, d_range, d_group,
                      (const uint32_t*)R.S.as<uint32_t>(), (const uint8_t*)R.pk_usable.as<uint8_t>(),
                      R.rec_code.as<uint8_t>(), R.rec_inf.as<uint8_t>(), R.rec_sig.as<uint32_t>(),
@@ -162,6 +358,8 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   R.valid = false;
   R.per_sig = false;
   R.K = 0;
+  R.pts = R.pq = R.aos = R.have_pos = false;
+  R.index_hi = index_hi;
   auto gt_one = [&]() {
     if (gt_out) {   // the empty product: Gt one
       memset(gt_out, 0, 576);
@@ -177,46 +375,13 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   int r = order_begin(c, s);
   if (r) return r;
   // 1. key groups (dedup of the 96-byte encodings; open addressing on a
-  //    64-bit hash, full compare) and a counting sort by group
+  //    64-bit hash, full compare) and a counting sort by group.  Slices of the
+  //    batch are deduplicated on host threads, then their distinct keys are
+  //    merged in slice order, so group ids follow first occurrence exactly as
+  //    a sequential pass would number them.
   std::vector<uint32_t> grp(n);
   std::vector<uint64_t> first;
-  {
-    auto khash = [](const uint8_t* k) {
-      uint64_t h = 0x9E3779B97F4A7C15ull;
-      for (int q = 0; q < 96; q += 8) {
-        uint64_t w;
-        memcpy(&w, k + q, 8);
-        h = (h ^ w) * 0xff51afd7ed558ccdull;
-        h ^= h >> 29;
-      }
-      return h;
-    };
-    std::vector<uint32_t> slot(64, 0);   // group id + 1; 0 = empty
-    uint64_t mask = 63;
-    for (uint64_t i = 0; i < n; i++) {
-      const uint8_t* k = pks + 96 * i;
-      uint64_t h = khash(k) & mask;
-      while (slot[h] && memcmp(pks + 96 * first[slot[h] - 1], k, 96) != 0) h = (h + 1) & mask;
-      if (!slot[h]) {
-        first.push_back(i);
-        slot[h] = (uint32_t)first.size();
-        if (2 * first.size() > mask) {   // grow and rehash
-          std::vector<uint32_t> ns(2 * (mask + 1), 0);
-          const uint64_t nm = 2 * (mask + 1) - 1;
-          for (uint32_t g = 0; g < first.size(); g++) {
-            uint64_t q = khash(pks + 96 * first[g]) & nm;
-            while (ns[q]) q = (q + 1) & nm;
-            ns[q] = g + 1;
-          }
-          slot.swap(ns);
-          mask = nm;
-        }
-        grp[i] = (uint32_t)first.size() - 1;
-      } else {
-        grp[i] = slot[h] - 1;
-      }
-    }
-  }
+  group_keys(pks, n, grp, first);
   const uint32_t K = R.K = (uint32_t)first.size();
   // 1b. many distinct keys: a combination needs K + 1 pairings anyway and a
   //     forgery's bisection would cost more than per-signature verification,
@@ -238,9 +403,18 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     std::vector<uint64_t> pos(R.gbeg.begin(), R.gbeg.end() - 1);
     for (uint64_t i = 0; i < n; i++) R.perm[pos[grp[i]]++] = (uint32_t)i;
   }
-  // 2. device buffers
+  // 2. device buffers (bucket path: the batch's points and codes stay on the
+  //    device for msm_sums; per-record multiples only if bisection needs them)
+  R.pts = msm_ok(n, (uint64_t)K + 1);
+  R.pq = !R.pts;
   r = 0;
-  r |= R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4) | R.d_perm.ensure(n * 4) | R.d_seed.ensure(32);
+  if (R.pts) {
+    r |= R.Xs.ensure(n * CESS_W_G1 * 4) | R.Xh.ensure(n * CESS_W_G1 * 4) | R.d_code.ensure(n) | R.d_inf.ensure(n);
+    r |= R.d_grp.ensure(n * 4);
+  } else {
+    r |= R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4);
+  }
+  r |= R.d_perm.ensure(n * 4) | R.d_seed.ensure(32);
   r |= R.pk_in.ensure((uint64_t)K * 96);
   r |= R.pk_code.ensure(K) | R.pk_inf.ensure(K) | R.pk_aff.ensure((uint64_t)K * CESS_W_G2 * 4);
   r |= R.pk_coeffs.ensure((uint64_t)K * CESS_W_COEFFS * 4) | R.pk_usable.ensure(K);
@@ -254,6 +428,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     HIPCHK(hipStreamSynchronize(s));   // sw is a stack buffer
   }
   HIPCHK(hipMemcpyAsync(R.d_perm.p, R.perm.data(), n * 4, hipMemcpyHostToDevice, s));
+  if (R.pts) HIPCHK(hipMemcpyAsync(R.d_grp.p, grp.data(), n * 4, hipMemcpyHostToDevice, s));
   // 3. distinct keys: decode (G2Affine::from_compressed, src/lib.rs:74) + G2Prepared (:88), once per key
   std::vector<uint8_t> kbytes((uint64_t)K * 96), pkc(K), pki(K), usable(K);
   for (uint32_t g = 0; g < K; g++) memcpy(&kbytes[96 * (uint64_t)g], pks + 96 * first[g], 96);
@@ -293,8 +468,12 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
     const unsigned g = grid_for(m);
     StageSlot& S = c->slot[0];
+    // the points go to the batch-wide arrays (stride n) on the bucket path
+    uint32_t* sig_dst = R.pts ? R.Xs.as<uint32_t>() + off : S.sig_aff.as<uint32_t>();
+    uint32_t* h_dst = R.pts ? R.Xh.as<uint32_t>() + off : S.h_aff.as<uint32_t>();
+    const uint64_t pstride = R.pts ? n : c->qcap;
     hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
-                       c->code.as<uint8_t>(), S.inf.as<uint8_t>(), S.sig_aff.as<uint32_t>(), c->qcap);
+                       c->code.as<uint8_t>(), S.inf.as<uint8_t>(), sig_dst, pstride);
     HIPCHK(hipGetLastError());
     hc.resize(m);
     hi.resize(m);
@@ -311,11 +490,16 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     HIPCHK(hipMemcpyAsync(c->code.p, hc.data(), m, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(S.inf.p, hi.data(), m, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
-                       (const uint8_t*)c->code.as<uint8_t>(), S.h_aff.as<uint32_t>(), c->qcap);
-    hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)c->code.as<uint8_t>(),
-                       (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
-                       (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(),
-                       index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->qcap, (uint64_t)n);
+                       (const uint8_t*)c->code.as<uint8_t>(), h_dst, pstride);
+    if (R.pts) {
+      HIPCHK(hipMemcpyAsync(R.d_code.as<uint8_t>() + off, hc.data(), m, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(R.d_inf.as<uint8_t>() + off, hi.data(), m, hipMemcpyHostToDevice, s));
+    } else {
+      hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)c->code.as<uint8_t>(),
+                         (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
+                         (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(),
+                         index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->qcap, (uint64_t)n);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // hc/hi are reused by the next chunk
   }

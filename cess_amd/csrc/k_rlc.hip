@@ -8,7 +8,9 @@
 // (src/lib.rs:85-100), except with probability <= 2^-127 over the 128-bit r_i.
 // Malformed encodings never enter the sums: they keep their decode codes.
 //
-// k_rlc_scale  : P_i = r_i sig_i, Q_i = r_i H(m_i)   (r_i = SHA-256(seed || i)[0:16] | 1)
+// k_msm_*      : the sums of a check by buckets (Pippenger), the default path
+// k_rlc_scale  : P_i = r_i sig_i, Q_i = r_i H(m_i)   (r_i = SHA-256(seed || i)[0:16] | 1),
+//                for checks with too many segments for the bucket tables
 // k_g1_sum_segs    : segmented sums of projective G1 points over permuted index ranges
 // k_rlc_pairs_list : (range, key group) terms -> affine Miller-loop records (k_miller input)
 // k_fp12_prod_segs : per-range product of the terms' Miller-loop values
@@ -101,6 +103,212 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   }
   st_g1p(P, out_stride, i, p);
   st_g1p(Q, out_stride, i, q);
+}
+
+// ---- bucket (Pippenger) sums of a check --------------------------------------
+// A check needs only its segments' sums -- the batch's first check K + 1 of
+// them: sum_i r_i sig_i and, per key group g, sum_{i in g} r_i H(m_i) -- so
+// instead of one 128-bit scalar multiple per point (k_rlc_scale: 128
+// doublings + 64 additions) the scalars are cut into 16 windows of 8 bits and
+// each point is ADDED into one bucket per non-zero window digit: bucket b =
+// (seg * 16 + w) * 256 + d (MsmSegs: which segments a record's signature and
+// hash belong to).  Then W(seg, w) = sum_d d B(seg, w, d) (running sums), and
+// S(seg) = sum_w 2^(8w) W(seg, w).  About 16 mixed additions per point instead
+// of ~190 point operations (k_rlc_scale: 63 ms per 1 M records).  The sums
+// are the same group elements, so every check and its Gt value are unchanged.
+constexpr uint32_t MSM_WIN = 16, MSM_DIG = 256, MSM_SEG = MSM_WIN * MSM_DIG;
+
+__device__ __forceinline__ uint32_t msm_digit(const uint32_t (&k)[4], uint32_t w) {
+  return (k[w >> 2] >> (8 * (w & 3))) & 255u;   // k[0] is the least significant word
+}
+
+// index of the range [lo[a], hi[a]) holding position p, or -1 (lo sorted)
+__device__ __forceinline__ int msm_find(const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t cnt,
+                                        uint32_t p) {
+  if (cnt == 0 || p < lo[0]) return -1;
+  uint32_t a = 0, b = cnt;
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (lo[m] <= p) a = m;
+    else b = m;
+  }
+  return p < hi[a] ? (int)a : -1;
+}
+
+
+// every (bucket, record) entry of the valid records: counts (SCATTER false) or
+// the bucket-sorted record list idx (SCATTER true, ctr = per-bucket cursors
+// starting at the buckets' offsets)
+template <bool SCATTER>
+__device__ __forceinline__ void msm_bin(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                        const MsmSegs& sg, const uint32_t* __restrict__ seed, uint64_t index_base,
+                                        uint32_t* __restrict__ ctr, uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || code[i] != 0) return;
+  int seg[2];
+  if (!sg.pos) {
+    seg[0] = 0;
+    seg[1] = 1 + (int)sg.grp[i];
+  } else {
+    const uint32_t p = sg.pos[i];
+    seg[0] = msm_find(sg.plo, sg.phi, sg.nparts, p);
+    const int t = msm_find(sg.tlo, sg.thi, sg.nterms, p);
+    seg[1] = t < 0 ? -1 : (int)sg.nparts + t;
+  }
+  if (seg[0] < 0 && seg[1] < 0) return;   // outside this check's ranges
+  uint32_t k[4];
+  rlc_scalar(seed, index_base + i, k);
+  const uint8_t fl = inf[i];
+#pragma unroll 1
+  for (int set = 0; set < 2; set++) {
+    if (seg[set] < 0 || (fl & (set ? INF_PK : INF_SIG))) continue;   // an identity term contributes nothing
+    const uint32_t base = (uint32_t)seg[set] * MSM_SEG;
+#pragma unroll 1
+    for (uint32_t w = 0; w < MSM_WIN; w++) {
+      const uint32_t d = msm_digit(k, w);
+      if (!d) continue;
+      if (SCATTER)
+        idx[atomicAdd(&ctr[base + w * MSM_DIG + d], 1u)] = (uint32_t)i;
+      else
+        atomicAdd(&ctr[base + w * MSM_DIG + d], 1u);
+    }
+  }
+}
+
+__global__ CESS_LB void k_msm_count(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                    MsmSegs sg, const uint32_t* __restrict__ seed, uint64_t index_base,
+                                    uint32_t* __restrict__ counts) {
+  msm_bin<false>(n, code, inf, sg, seed, index_base, counts, nullptr);
+}
+__global__ CESS_LB void k_msm_scatter(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                      MsmSegs sg, const uint32_t* __restrict__ seed, uint64_t index_base,
+                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ idx) {
+  msm_bin<true>(n, code, inf, sg, seed, index_base, cursor, idx);
+}
+
+// pos[perm[j]] = j
+__global__ void k_inv_perm(uint64_t n, const uint32_t* __restrict__ perm, uint32_t* __restrict__ pos) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) pos[perm[j]] = (uint32_t)j;
+}
+
+// The batch's affine points record-major (24 words = 96 B per record), for
+// the bucket gathers: a record's point is then 6 x 16-byte loads from two
+// cache lines, where the SoA stage layout spreads it over 24 lines.
+__global__ CESS_LB void k_msm_aos(uint64_t n, const uint32_t* __restrict__ X, uint4* __restrict__ Xa) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[24];
+#pragma unroll
+  for (int k = 0; k < 24; k++) w[k] = X[(uint64_t)k * n + i];
+#pragma unroll
+  for (int q = 0; q < 6; q++) Xa[6 * i + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+struct AffPt {
+  uint4 v[6];
+};
+__device__ __forceinline__ AffPt ld_aff(const uint4* __restrict__ Xa, uint32_t i) {
+  AffPt p;
+#pragma unroll
+  for (int q = 0; q < 6; q++) p.v[q] = Xa[6 * (uint64_t)i + q];
+  return p;
+}
+__device__ __forceinline__ void aff_xy(const AffPt& p, fp& x, fp& y) {
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    x.v[4 * q] = p.v[q].x, x.v[4 * q + 1] = p.v[q].y, x.v[4 * q + 2] = p.v[q].z, x.v[4 * q + 3] = p.v[q].w;
+    y.v[4 * q] = p.v[3 + q].x, y.v[4 * q + 1] = p.v[3 + q].y, y.v[4 * q + 2] = p.v[3 + q].z, y.v[4 * q + 3] = p.v[3 + q].w;
+  }
+}
+
+// Work item j = one chunk of one bucket's entries (msm_chunk: >= 64 entries,
+// <= 32 chunks per bucket; item_off = the buckets' first items, host-built):
+// the chunk's points summed with mixed additions (record-major affine points,
+// k_msm_aos; the parts' segments read the signatures Xs, the terms' the
+// hashes Xh), the
+// next entry's point loaded while the current one is added.
+__global__ CESS_LB void k_msm_items(uint32_t n_items, uint32_t nb, uint32_t nparts, const uint32_t* __restrict__ item_off,
+                                    const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bcnt,
+                                    const uint32_t* __restrict__ idx, const uint4* __restrict__ Xs,
+                                    const uint4* __restrict__ Xh, uint32_t* __restrict__ part, uint64_t pstride) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_items) return;
+  uint32_t lo = 0, hi = nb;   // the last bucket whose first item is <= j (non-empty)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (item_off[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t b = lo, cnt = bcnt[b], L = msm_chunk(cnt), t = j - item_off[b];
+  const uint32_t s = bstart[b] + t * L, e = bstart[b] + min(cnt, (t + 1) * L);
+  const uint4* X = b < nparts * MSM_SEG ? Xs : Xh;   // parts: signatures; terms: hashes
+  g1p acc = proj_identity<fp>();
+  AffPt nxt = ld_aff(X, idx[s]);
+#pragma unroll 1
+  for (uint32_t q = s; q < e; q++) {
+    const AffPt cur = nxt;
+    if (q + 1 < e) nxt = ld_aff(X, idx[q + 1]);
+    fp x, y;
+    aff_xy(cur, x, y);
+    acc = proj_add_mixed(acc, x, y);
+  }
+  st_g1p(part, pstride, j, acc);
+}
+
+// bucket b = the sum of its items' partials (at most 32)
+__global__ CESS_LB void k_msm_bucket_sum(uint32_t nb, const uint32_t* __restrict__ item_off,
+                                         const uint32_t* __restrict__ part, uint64_t pstride,
+                                         uint32_t* __restrict__ bsum) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (uint32_t j = item_off[b]; j < item_off[b + 1]; j++) acc = proj_add(acc, ld_g1p(part, pstride, j));
+  st_g1p(bsum, nb, b, acc);
+}
+
+// lane t = (seg * 16 + w) * 16 + q: sum_{d in [16q, 16q + 16)} d B(seg, w, d)
+// by a running sum over the 16 digits (B(., ., 0) is empty)
+__global__ CESS_LB void k_msm_window(uint32_t nseg, const uint32_t* __restrict__ bsum, uint64_t nb,
+                                     uint32_t* __restrict__ T) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = nseg * MSM_WIN * 16;
+  if (t >= nt) return;
+  const uint32_t sw = t >> 4, q = t & 15;
+  g1p acc = proj_identity<fp>(), sum = proj_identity<fp>();
+#pragma unroll 1
+  for (int d = 16 * (int)q + 15; d >= 16 * (int)q; d--) {
+    if (d) acc = proj_add(acc, ld_g1p(bsum, nb, sw * MSM_DIG + (uint32_t)d));
+    sum = proj_add(sum, acc);
+  }
+  // sum = sum_d (d - 16q + 1) B_d, acc = sum_d B_d: add (16q - 1) acc
+  const g1p corr = q ? proj_mul_u64(acc, 16 * q - 1) : proj_neg(acc);
+  st_g1p(T, nt, t, proj_add(sum, corr));
+}
+
+// lane (seg, w): U(seg, w) = 2^(8w) sum_q T(seg, w, q)
+__global__ CESS_LB void k_msm_wsum(uint32_t nseg, const uint32_t* __restrict__ T, uint32_t* __restrict__ U) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nu = nseg * MSM_WIN, nt = nu * 16;
+  if (t >= nu) return;
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (uint32_t q = 0; q < 16; q++) acc = proj_add(acc, ld_g1p(T, nt, t * 16 + q));
+#pragma unroll 1
+  for (uint32_t r = 0; r < 8 * (t % MSM_WIN); r++) acc = proj_dbl(acc);
+  st_g1p(U, nu, t, acc);
+}
+
+// lane seg: S(seg) = sum_w U(seg, w); parts -> S[seg] (stride nparts), terms
+// -> Qs[seg - nparts] (stride nterms)
+__global__ CESS_LB void k_msm_finish(uint32_t nseg, uint32_t nparts, const uint32_t* __restrict__ U,
+                                     uint32_t* __restrict__ S, uint32_t* __restrict__ Qs) {
+  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x, nu = nseg * MSM_WIN;
+  if (sg >= nseg) return;
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (uint32_t w = 0; w < MSM_WIN; w++) acc = proj_add(acc, ld_g1p(U, nu, sg * MSM_WIN + w));
+  if (sg < nparts) st_g1p(S, nparts, sg, acc);
+  else st_g1p(Qs, nseg - nparts, sg - nparts, acc);
 }
 
 // Segmented sums (batched bisection): segment q = perm positions

@@ -30,3 +30,25 @@ enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
 #define CESS_W_FP12 144u
 #define CESS_FE_SLOTS 15u      // HBM Fp12 slots of the final-exponentiation program (bls/staged.hpp):
                                // 7 temporaries, 6 powers of FE_CHAIN, 2 ping-pong accumulators
+
+// RLC bucket sums (k_rlc.hip k_msm_*): 16 windows x 256 digit buckets per
+// segment; a bucket of cnt entries is summed in chunks of msm_chunk(cnt)
+// entries (at least 64, at most 32 chunks), one work item per chunk
+#define CESS_MSM_SEG_BUCKETS 4096u
+#define CESS_MSM_MAX_SEGS 1024u   // segments of one bucket pass (bucket tables <= 4 M entries)
+// Segments of one bucket pass (kernel argument): parts (perm-position ranges;
+// their signatures) are segments 0 .. nparts - 1, terms (part x key group
+// ranges; their hashes) nparts + t.  pos == nullptr: the batch's first check
+// (one part = the whole batch, term g = key group g: segment 1 + grp[i]); else
+// pos[i] = record i's perm position, looked up in the sorted bounds.
+struct MsmSegs {
+  const uint32_t *grp, *pos, *plo, *phi, *tlo, *thi;
+  uint32_t nparts, nterms;
+};
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t msm_chunk(uint32_t cnt) {
+  const uint32_t c = (cnt + 31u) / 32u;
+  return c > 64u ? c : 64u;
+}

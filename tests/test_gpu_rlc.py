@@ -2,12 +2,28 @@
 4 shape: few keys).  Parity bar: the per-record codes equal the per-signature
 path's (cess_bls_verify_batch) on the same records, including forged,
 malformed, non-subgroup and identity inputs, and the cross-shard Gt-product
-combine gives the same verdicts as one shard."""
+combine gives the same verdicts as one shard.  Every test runs with the
+first check's sums from the bucket kernels (k_msm_*, env CESS_BLS_RLC_MSM=1)
+and from per-record scalar multiples (=0); the Gt value of a failing check is
+the same group element either way (test_rlc_bucket_sums_equal_scalar_multiples)."""
+import os
 import random
 
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["msm", "scale"])
+def rlc_sums_path(request):
+    old = os.environ.get("CESS_BLS_RLC_MSM")
+    os.environ["CESS_BLS_RLC_MSM"] = "1" if request.param == "msm" else "0"
+    yield request.param
+    if old is None:
+        os.environ.pop("CESS_BLS_RLC_MSM", None)
+    else:
+        os.environ["CESS_BLS_RLC_MSM"] = old
+
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 
@@ -96,3 +112,68 @@ def test_rlc_empty_and_tiny(ctx):
     msgs[1] = bytes(32)
     codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(32))
     assert list(codes) == [0, 5, 0]
+
+
+def test_rlc_bucket_sums_equal_scalar_multiples(ctx, vectors, rlc_sums_path):
+    """The Gt value of one failing combination (forgery, malformed and identity
+    records in it) is bit-identical whether the sums come from the buckets or
+    from per-record multiples, with several key groups and 20,000 records."""
+    if rlc_sums_path != "msm":
+        pytest.skip("compares both paths itself")
+    sigs, pks, msgs = _few_key_batch(ctx, 20000, 6, 7)
+    msgs[777] = bytes(32)                                        # forgery
+    sigs[1234] = b"\xc0" + bytes(47)                             # identity signature
+    sigs[4321] = bytes([sigs[4321][0] & 0x7F]) + sigs[4321][1:]  # malformed
+    cases = [c for c in vectors["cases"] if len(bytes.fromhex(c["sig"])) == 48 and len(bytes.fromhex(c["pk"])) == 96]
+    for j, c in zip(range(5000, 20000, 2500), cases):
+        sigs[j], msgs[j], pks[j] = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+    packed = _pack(sigs, pks, msgs)
+    seed = bytes(range(100, 132))
+    gts, codes, stats = {}, {}, {}
+    for mode in ("1", "0"):
+        os.environ["CESS_BLS_RLC_MSM"] = mode
+        gts[mode] = ctx.rlc_begin(*packed, seed=seed)
+        codes[mode], _, stats[mode] = ctx.rlc_finish(False)
+    one = bytes(47) + b"\x01" + bytes(576 - 48)
+    assert gts["1"] == gts["0"] != one
+    # every bisection check decides the same way on both paths (a wrong
+    # sub-range sum would fail a check the other path passes)
+    assert stats["1"] == stats["0"] and stats["1"]["checks"] > 1
+    expect, _ = ctx.verify_fixed(*packed)
+    assert codes["1"] == codes["0"] == expect
+    assert expect[777] == 5 and expect[4321] != 0 and expect.count(0) < 20000 - 3
+
+
+def test_rlc_bucket_path_large_batch(ctx, rlc_sums_path):
+    """Default selection (env unset) on a batch large enough for the buckets
+    and for the threaded key grouping (>= 2 slices of 65,536): all valid ->
+    one check (a wrong group id would fail it), all codes 0; one forgery ->
+    exactly that record fails."""
+    if rlc_sums_path != "msm":
+        pytest.skip("one run suffices")
+    del os.environ["CESS_BLS_RLC_MSM"]
+    sigs, pks, msgs = _few_key_batch(ctx, 140000, 4, 8)
+    codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(32))
+    assert set(codes) == {0} and st["checks"] == 1 and st["distinct_keys"] == 4
+    msgs[123456] = bytes(32)
+    codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(32))
+    assert codes[123456] == 5 and codes.count(0) == 139999
+    # one forgery: one failing range per level, so one leaf (16 + 5 checks below the first)
+    assert st["leaves"] == 1 and st["checks"] == 1 + 16 + 5, st
+
+
+def test_rlc_points_kept_scalar_multiple_fallback(ctx, rlc_sums_path):
+    """Default selection with 141 segments for 9,000 records (< 64 records per
+    segment): the points are kept on the device but the check takes the
+    per-record multiples (computed from them); codes stay exact."""
+    if rlc_sums_path != "msm":
+        pytest.skip("one run suffices")
+    del os.environ["CESS_BLS_RLC_MSM"]
+    sigs, pks, msgs = _few_key_batch(ctx, 9000, 140, 9)
+    msgs[10] = bytes(32)
+    msgs[8000] = bytes(32)
+    packed = _pack(sigs, pks, msgs)
+    expect, _ = ctx.verify_fixed(*packed)
+    codes, words, st = ctx.verify_rlc(*packed, seed=bytes(32))
+    assert codes == expect and codes[10] == 5 and codes[8000] == 5 and codes.count(0) == 8998
+    assert st["distinct_keys"] == 140 and st["checks"] > 1

@@ -190,7 +190,11 @@ int cess_bls_gt_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const ui
  * whose errors cancel in the combination and the batch reports them valid.
  * Pass seed32 = NULL to have the library draw one from the OS CSPRNG
  * (getrandom(2)).  Batches with more than one distinct key per 8 records gain
- * nothing from a combination and are verified per signature. */
+ * nothing from a combination and are verified per signature.
+ * The sums of a check are formed by 8-bit-window buckets (Pippenger) when the
+ * check has at most 1,024 segments and 64 records per segment, else from each
+ * record's multiples; env CESS_BLS_RLC_MSM=0 forces the latter, =1 the buckets
+ * whenever the tables fit (tests).  Both give the same group elements. */
 int cess_bls_verify_batch_rlc(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks,
                               const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
                               uint8_t* codes_out, uint64_t* bitmap_out,

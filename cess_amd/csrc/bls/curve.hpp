@@ -228,6 +228,90 @@ CESS_HD proj<F> proj_mul_scalar_mixed(const F& px, const F& py, const uint32_t (
   return acc;
 }
 
+// GLV split of a scalar for G1, where r = L^2 + L + 1 with L = x^2 - 1 (128
+// bits) and [L]P = (beta^2 x, y) (beta: c::G1_BETA, phi = [-x^2] = [L^2];
+// batch signing, k_sign.hip):
+// k mod r = k1 + k2 L with 0 <= k1 < L and k2 < 2^128 -- plain long division
+// by L (k is first reduced below r; a 32-byte key may exceed it).  Words
+// little-endian.
+CESS_CONST uint32_t R_LE[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                              0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+CESS_CONST uint32_t LAMBDA_LE[4] = {0xffffffffu, 0x00000000u, 0x0001a402u, 0xac45a401u};
+
+CESS_HD void sub_r_if_ge(uint32_t (&k)[8]) {
+  uint32_t t[8], br = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) t[w] = subc32(k[w], R_LE[w], br, &br);
+#pragma unroll
+  for (int w = 0; w < 8; w++) k[w] = br ? k[w] : t[w];
+}
+
+CESS_HD void glv_split(const uint32_t (&k0)[8], uint32_t (&k1)[4], uint32_t (&k2)[4]) {
+  uint32_t k[8];
+#pragma unroll
+  for (int w = 0; w < 8; w++) k[w] = k0[w];
+  sub_r_if_ge(k);
+  sub_r_if_ge(k);   // 2^256 < 3 r
+  uint32_t rem[5] = {0, 0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+#pragma unroll 1
+  for (int bit = 255; bit >= 0; bit--) {
+    // rem = 2 rem + bit (rem < L before, so < 2^129), q <<= 1
+#pragma unroll
+    for (int w = 4; w > 0; w--) rem[w] = (rem[w] << 1) | (rem[w - 1] >> 31);
+    rem[0] = (rem[0] << 1) | ((k[bit >> 5] >> (bit & 31)) & 1u);
+#pragma unroll
+    for (int w = 3; w > 0; w--) q[w] = (q[w] << 1) | (q[w - 1] >> 31);
+    q[0] <<= 1;
+    uint32_t t[5], br = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) t[w] = subc32(rem[w], LAMBDA_LE[w], br, &br);
+    t[4] = subc32(rem[4], 0u, br, &br);
+    const bool ge = br == 0;
+#pragma unroll
+    for (int w = 0; w < 5; w++) rem[w] = ge ? t[w] : rem[w];
+    q[0] |= ge ? 1u : 0u;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) k1[w] = rem[w], k2[w] = q[w];
+}
+
+// [k]P for affine P in G1 (not the identity): [k1]P + [k2]([L]P) by 2-bit
+// joint windows over the affine table {P, 2P, 3P} (one inversion) and its
+// image (beta^2 x, y): 128 doublings + 128 complete mixed additions, against
+// 256 doublings + 256 additions for the bitwise ladder (some lane of a wave
+// always adds).  The additions are computed every window and kept by a select
+// (digits differ per lane).
+CESS_HD g1p g1_mul_glv(const fp& px, const fp& py, const uint32_t (&k)[8]) {
+  uint32_t k1[4], k2[4];
+  glv_split(k, k1, k2);
+  const g1p P2 = proj_dbl(g1p{px, py, fp_one()});
+  const g1p P3 = proj_add_mixed(P2, px, py);
+  const fp zi = inv(mul(P2.z, P3.z));
+  const fp z2i = mul(zi, P3.z), z3i = mul(zi, P2.z);
+  const fp x2 = mul(P2.x, z2i), y2 = mul(P2.y, z2i), x3 = mul(P3.x, z3i), y3 = mul(P3.y, z3i);
+  const fp beta = fp_from(c::G1_BETA);
+  const fp beta2 = mul(beta, beta);
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (int w = 63; w >= 0; w--) {
+    acc = proj_dbl(proj_dbl(acc));
+    const int sh = 2 * (w & 15);
+    const uint32_t d1 = (k1[w >> 4] >> sh) & 3u, d2 = (k2[w >> 4] >> sh) & 3u;
+    {
+      const fp tx = select(d1 == 1, px, select(d1 == 2, x2, x3)), ty = select(d1 == 1, py, select(d1 == 2, y2, y3));
+      const g1p s = proj_add_mixed(acc, tx, ty);
+      acc = {select(d1 != 0, s.x, acc.x), select(d1 != 0, s.y, acc.y), select(d1 != 0, s.z, acc.z)};
+    }
+    {
+      const fp tx = mul(select(d2 == 1, px, select(d2 == 2, x2, x3)), beta2);
+      const fp ty = select(d2 == 1, py, select(d2 == 2, y2, y3));
+      const g1p s = proj_add_mixed(acc, tx, ty);
+      acc = {select(d2 != 0, s.x, acc.x), select(d2 != 0, s.y, acc.y), select(d2 != 0, s.z, acc.z)};
+    }
+  }
+  return acc;
+}
+
 // ---------------------------------------------------------------------------
 // subgroup checks
 // ---------------------------------------------------------------------------

@@ -58,6 +58,16 @@ void emu_clear_cofactor(const uint32_t* x, const uint32_t* y, uint32_t* out, int
   store_raw(r.x, out);
   store_raw(r.y, out + 12);
 }
+// [k]P by curve.hpp g1_mul_glv (k: 8 little-endian words) for a raw affine
+// point P of G1
+void emu_g1_mul_glv(const uint32_t* x, const uint32_t* y, const uint32_t* k, uint32_t* out, int* inf) {
+  uint32_t kk[8];
+  memcpy(kk, k, 32);
+  g1a r = proj_to_affine(g1_mul_glv(to_mont(load_raw(x)), to_mont(load_raw(y)), kk));
+  *inf = r.inf;
+  store_raw(r.x, out);
+  store_raw(r.y, out + 12);
+}
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
 // safegcd inverse of a Montgomery-domain value in [0, 2p); out canonical Montgomery
 void emu_fp_inv_mont(const uint32_t* a, uint32_t* out) {
@@ -168,7 +178,7 @@ void emu_opcount_sign(const uint8_t* sk, const uint8_t* msg, uint32_t mlen, uint
   }
   g_mul_count = g_sqr_count = g_mul2_count = g_half_count = 0;
   g1a h = hash_to_g1(msg, mlen);
-  g1a s = proj_to_affine(proj_mul_scalar_mixed(h.x, h.y, k));
+  g1a s = proj_to_affine(g1_mul_glv(h.x, h.y, k));
   uint8_t b[48];
   g1_compress(s, b);
   out[0] = 2 * g_mul_count + 5 * g_mul2_count + g_half_count;   // half-multiplies

@@ -90,6 +90,31 @@ def test_clear_cofactor_jacobian(emu):
             assert inf.value == 0 and got == want, (x, y)
 
 
+def test_g1_mul_glv(emu):
+    """curve.hpp g1_mul_glv (batch signing): the GLV split k mod r = k1 + k2 L
+    (L = x^2 - 1) and the joint 2-bit windows equal the oracle's [k mod r]P at
+    the split's edges, for keys >= r, and on random keys and points of G1."""
+    import random
+
+    import oracle.bls_oracle as o
+    rng = random.Random(31)
+    L = o.X * o.X - 1
+    limbs = lambda v, n: (ctypes.c_uint32 * n)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)])
+    ks = [0, 1, 2, 3, L - 1, L, L + 1, L * L, L * L + L, 1 << 128, o.R - 1, o.R, o.R + 1, (1 << 256) - 1]
+    ks += [rng.randrange(1 << 256) for _ in range(6)] + [rng.randrange(o.R) for _ in range(6)]
+    for j, k in enumerate(ks):
+        pt = o.ec_mul(o.FP, o.G1_GEN, rng.randrange(1, o.R)) if j % 3 else o.G1_GEN
+        out = (ctypes.c_uint32 * 24)()
+        inf = ctypes.c_int()
+        emu.emu_g1_mul_glv(limbs(pt[0], 12), limbs(pt[1], 12), limbs(k, 8), out, ctypes.byref(inf))
+        want = o.ec_mul(o.FP, pt, k % o.R)
+        if want is None:
+            assert inf.value == 1, hex(k)
+        else:
+            got = (sum(out[i] << (32 * i) for i in range(12)), sum(out[12 + i] << (32 * i) for i in range(12)))
+            assert inf.value == 0 and got == want, hex(k)
+
+
 def test_staged_matches_valuebased(emu, vectors):
     """The staged Fp12 code (LDS/HBM stores, final-exponentiation program) gives
     the same Gt as the value-based Fp12 code on every golden record."""

@@ -177,3 +177,18 @@ def test_rlc_points_kept_scalar_multiple_fallback(ctx, rlc_sums_path):
     codes, words, st = ctx.verify_rlc(*packed, seed=bytes(32))
     assert codes == expect and codes[10] == 5 and codes[8000] == 5 and codes.count(0) == 8998
     assert st["distinct_keys"] == 140 and st["checks"] > 1
+
+
+def test_rlc_repeated_records(ctx, rlc_sums_path):
+    """One record repeated 12,000 times among 8,000 others: a bucket then
+    adds the same point to itself (the complete formulas' doubling case) and
+    the check must still pass; a forged copy of it must still be isolated."""
+    sigs, pks, msgs = _few_key_batch(ctx, 8000, 3, 12)
+    sigs += [sigs[5]] * 12000
+    pks += [pks[5]] * 12000
+    msgs += [msgs[5]] * 12000
+    codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(range(32)))
+    assert set(codes) == {0} and st["checks"] == 1
+    msgs[15000] = bytes(32)
+    codes, words, st = ctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(range(32)))
+    assert codes[15000] == 5 and codes.count(0) == 19999

@@ -34,6 +34,7 @@ pub const CESS_BLS_F_STRICT_IDENTITY: u32 = 2;
 pub const CESS_BLS_MODE_PER_SIG: u32 = 0;
 pub const CESS_BLS_MODE_RLC: u32 = 1;
 pub const CESS_BLS_COMM_ID_BYTES: usize = 128;
+pub const CESS_BLS_BUS_ID_BYTES: usize = 32;
 
 #[repr(C)]
 pub struct cess_bls_config {
@@ -120,6 +121,12 @@ extern "C" {
     pub fn cess_bls_comm_barrier(ctx: *mut cess_bls_ctx) -> c_int;
     pub fn cess_bls_comm_max_f64(ctx: *mut cess_bls_ctx, value: *mut f64) -> c_int;
     pub fn cess_bls_comm_kind(ctx: *mut cess_bls_ctx) -> *const c_char;
+    pub fn cess_bls_comm_info(ctx: *mut cess_bls_ctx, nranks_out: *mut c_int, rank_out: *mut c_int,
+                              bus_ids_out: *mut c_char) -> c_int;
+    pub fn cess_bls_verify_batch_var_sharded(ctx: *mut cess_bls_ctx, n: usize, sig_data: *const u8,
+                                             sig_offsets: *const u64, pk_data: *const u8, pk_offsets: *const u64,
+                                             msgs: *const u8, msg_offsets: *const u64, codes_out: *mut u8,
+                                             bitmap_out: *mut u64) -> c_int;
     // host shared-memory transport of the sharded entry points (ranks on one host)
     pub fn cess_bls_comm_shm_name(name_out: *mut c_char) -> c_int;
     pub fn cess_bls_comm_init_shm(ctx: *mut cess_bls_ctx, nranks: c_int, rank: c_int, name: *const c_char) -> c_int;
@@ -159,6 +166,9 @@ extern "C" {
     // diagnostics
     pub fn cess_bls_stage_times(ctx: *mut cess_bls_ctx, names: *mut *const c_char, ms: *mut f64, max: c_int,
                                 reset: c_int) -> c_int;
+    pub fn cess_bls_stage_stats(ctx: *mut cess_bls_ctx, names: *mut *const c_char, ms: *mut f64, launches: *mut u64,
+                                max: c_int, reset: c_int) -> c_int;
+    pub fn cess_bls_launch_records(ctx: *mut cess_bls_ctx) -> u64;
     pub fn cess_bls_status_string(status: c_int) -> *const c_char;
     pub fn cess_bls_version() -> *const c_char;
 

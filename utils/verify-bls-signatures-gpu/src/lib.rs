@@ -256,6 +256,35 @@ impl Verifier {
         })?;
         Ok(v)
     }
+    /// `verify_batch` over the communicator for records of any lengths: this
+    /// rank verifies its index shard, every rank receives all verdicts.
+    pub fn verify_batch_var_sharded(&mut self, records: &[(&[u8], &[u8], &[u8])]) -> Result<Verdicts, Error> {
+        let n = records.len();
+        let mut v = Verdicts { bitmap: vec![0; (n + 63) / 64], codes: vec![0; n] };
+        let (mut sd, mut pd, mut md) = (Vec::new(), Vec::new(), Vec::new());
+        let so = offsets(records.iter().map(|r| r.0), &mut sd);
+        let po = offsets(records.iter().map(|r| r.2), &mut pd);
+        let mo = offsets(records.iter().map(|r| r.1), &mut md);
+        check(unsafe {
+            ffi::cess_bls_verify_batch_var_sharded(self.ctx, n, sd.as_ptr(), so.as_ptr(), pd.as_ptr(), po.as_ptr(),
+                                                   md.as_ptr(), mo.as_ptr(), v.codes.as_mut_ptr(),
+                                                   v.bitmap.as_mut_ptr())
+        })?;
+        Ok(v)
+    }
+    /// What the communicator reports: (rank count, own rank, each rank's PCI
+    /// bus id in rank order).  Collective: call it on every rank.
+    pub fn comm_info(&mut self) -> Result<(i32, i32, Vec<String>), Error> {
+        let (mut nr, mut rk) = (0 as c_int, 0 as c_int);
+        check(unsafe { ffi::cess_bls_comm_info(self.ctx, &mut nr, &mut rk, core::ptr::null_mut()) })?;
+        let mut buf = vec![0 as core::ffi::c_char; nr.max(1) as usize * ffi::CESS_BLS_BUS_ID_BYTES];
+        check(unsafe { ffi::cess_bls_comm_info(self.ctx, &mut nr, &mut rk, buf.as_mut_ptr()) })?;
+        let ids = buf
+            .chunks(ffi::CESS_BLS_BUS_ID_BYTES)
+            .map(|c| unsafe { CStr::from_ptr(c.as_ptr()) }.to_string_lossy().into_owned())
+            .collect();
+        Ok((nr, rk, ids))
+    }
     /// Host shared-memory transport instead of RCCL (ranks on one host, which
     /// may share a GPU); `name` from `Verifier::comm_shm_name` on one rank.
     pub fn comm_init_shm(&mut self, nranks: i32, rank: i32, name: &CStr) -> Result<(), Error> {

@@ -13,11 +13,16 @@ product, checked by tests/test_patches.py with `git apply --check`.
 The patch changes (file: what):
   Cargo.toml                          workspace members += the two utils crates
   primitives/common/src/lib.rs        TeeBlsSignature = [u8; 48], TeeBlsPublicKey = [u8; 96]
-  c-pallets/tee-worker/src/lib.rs     TeeBlsKey storage, register_bls_key call, key removed on exit,
-                                      ScheduleFind::bls_key (default None: other implementors unchanged)
+  c-pallets/tee-worker/src/lib.rs     TeeBlsKey storage, register_bls_key call (the key must deserialize
+                                      as the reference crate's PublicKey: InvalidBlsKey otherwise), key
+                                      removed on exit, ScheduleFind::bls_key (default None: other
+                                      implementors unchanged)
+  c-pallets/tee-worker/Cargo.toml     dependency on ic-verify-bls-signature (the reference crate)
   c-pallets/audit/src/lib.rs          submit_verify_result verifies the TEE worker's BLS signature over
                                       the verdict (was `_tee_signature: NodeSignature`, unchecked,
-                                      "TODO! Podr2Key verify" at :480-484); verify_record / verify_result_message
+                                      "TODO! Podr2Key verify" at :480-484) with the non-panicking
+                                      runtime::verify_bls_signature; weight += WASM_VERIFY_BLS_WEIGHT;
+                                      verify_record / verify_result_message
   c-pallets/audit/Cargo.toml          dependency on cess-gpu-verify-runtime
   runtime/src/lib.rs                  spec_version / transaction_version bump (the call's encoding
                                       changes), decode_verify_record, GpuVerifyRecords runtime API
@@ -58,6 +63,10 @@ EDITS = {
          "pub type TeeBlsPublicKey = [u8; 96];\n"),
     ],
     "c-pallets/tee-worker/src/lib.rs": [
+        ("\t\tVerifyCertFailed,\n\t}\n",
+         "\t\tVerifyCertFailed,\n"
+         "\t\t//register_bls_key: the key is not a compressed point of G2\n"
+         "\t\tInvalidBlsKey,\n\t}\n"),
         ("\t\tUpdatePeerId { acc: AccountOf<T> },\n",
          "\t\tUpdatePeerId { acc: AccountOf<T> },\n\n\t\tRegisterBlsKey { acc: AccountOf<T> },\n"),
         ("\tpub(super) type TeePodr2Pk<T: Config> = StorageValue<_, Podr2Key>;\n",
@@ -73,12 +82,22 @@ EDITS = {
          "\t\t\tSelf::deposit_event(Event::<T>::Exit { acc: sender });\n\n\t\t\tOk(())\n\t\t}\n\n"
          "\t\t/// Register (or replace) the caller's BLS12-381 verdict key: 96 bytes,\n"
          "\t\t/// a compressed G2 point as ic-verify-bls-signature's PublicKey.\n"
+         "\t\t/// The key must deserialize as the reference crate's PublicKey\n"
+         "\t\t/// (utils/verify-bls-signatures/src/lib.rs:68-82: a point of G2), so a\n"
+         "\t\t/// stored key never makes a later verification fail on decoding.\n"
+         "\t\t/// Weight: 10_000_000 for the storage work + 5_000_000_000 (5 ms), a\n"
+         "\t\t/// conservative bound on one G2 decompression and subgroup check in\n"
+         "\t\t/// wasm, until this call has a FRAME benchmark.\n"
          "\t\t#[pallet::call_index(9)]\n"
          "\t\t#[transactional]\n"
-         "\t\t#[pallet::weight(10_000_000)]\n"
+         "\t\t#[pallet::weight(10_000_000 + 5_000_000_000)]\n"
          "\t\tpub fn register_bls_key(origin: OriginFor<T>, key: TeeBlsPublicKey) -> DispatchResult {\n"
          "\t\t\tlet sender = ensure_signed(origin)?;\n"
          "\t\t\tensure!(TeeWorkerMap::<T>::contains_key(&sender), Error::<T>::NonTeeWorker);\n"
+         "\t\t\tensure!(\n"
+         "\t\t\t\tic_verify_bls_signature::PublicKey::deserialize(&key).is_ok(),\n"
+         "\t\t\t\tError::<T>::InvalidBlsKey\n"
+         "\t\t\t);\n"
          "\t\t\tTeeBlsKey::<T>::insert(&sender, key);\n"
          "\t\t\tSelf::deposit_event(Event::<T>::RegisterBlsKey { acc: sender });\n"
          "\t\t\tOk(())\n"
@@ -95,6 +114,11 @@ EDITS = {
          "\t\tTeeBlsKey::<T>::get(acc)\n"
          "\t}\n}\n"),
     ],
+    "c-pallets/tee-worker/Cargo.toml": [
+        ("cp-enclave-verify = { path = '../../primitives/enclave-verify', version = '0.1.0', default-features = false }\n",
+         "cp-enclave-verify = { path = '../../primitives/enclave-verify', version = '0.1.0', default-features = false }\n"
+         "ic-verify-bls-signature = { path = '../../utils/verify-bls-signatures', version = '0.2.0', default-features = false }\n"),
+    ],
     "c-pallets/audit/src/lib.rs": [
         ("\t\tNonExistentMission,\n\n\t\tUnexpectedError,\n",
          "\t\tNonExistentMission,\n\n\t\tUnexpectedError,\n"
@@ -102,20 +126,27 @@ EDITS = {
          "\t\tNoTeeBlsKey,\n"
          "\t\t//The TEE worker's signature over the verdict does not verify\n"
          "\t\tVerifyTeeSigFailed,\n"),
+        ("\t\t#[pallet::weight(100_000_000)]\n\t\tpub fn submit_verify_result(",
+         "\t\t// Weight: the reference's 100_000_000 plus a conservative bound on the\n"
+         "\t\t// wasm BLS verification a node without a GPU verdict runs\n"
+         "\t\t// (cess_gpu_verify_runtime::WASM_VERIFY_BLS_WEIGHT), until this call has\n"
+         "\t\t// a FRAME benchmark with a signed verdict.\n"
+         "\t\t#[pallet::weight(100_000_000 + cess_gpu_verify_runtime::WASM_VERIFY_BLS_WEIGHT)]\n"
+         "\t\tpub fn submit_verify_result("),
         ("\t\t\t_tee_signature: NodeSignature,\n", "\t\t\ttee_signature: TeeBlsSignature,\n"),
         ("\t\t\t// TODO! Podr2Key verify\n",
          "\t\t\t// The TEE worker's BLS12-381 signature over the verdict and the\n"
-         "\t\t\t// challenge round it answers (ic-verify-bls-signature semantics):\n"
-         "\t\t\t// the MI355X batch verifier's host function answers from its\n"
-         "\t\t\t// verdict cache; a node without a GPU verdict runs the runtime's own\n"
-         "\t\t\t// cp_enclave_verify::verify_bls here, so every node agrees.\n"
-         "\t\t\t// Weight: the declared weight must cover that wasm verification (two\n"
-         "\t\t\t// pairings) -- re-run this call's FRAME benchmark with a signed verdict.\n"
+         "\t\t\t// challenge round it answers, with the total semantics of\n"
+         "\t\t\t// ic_verify_bls_signature::verify_bls_signature (a signature or key\n"
+         "\t\t\t// that does not deserialize is an Err, never a panic): the MI355X\n"
+         "\t\t\t// batch verifier's host function answers from its verdict cache, and\n"
+         "\t\t\t// a node without a GPU verdict runs that reference function in wasm,\n"
+         "\t\t\t// so every node reaches the same verdict.\n"
          "\t\t\tlet (sig, msg, key) =\n"
          "\t\t\t\tSelf::verify_record(&sender, &miner, idle_result, service_result, &tee_signature)\n"
          "\t\t\t\t\t.ok_or(Error::<T>::NoTeeBlsKey)?;\n"
          "\t\t\tensure!(\n"
-         "\t\t\t\tcess_gpu_verify_runtime::runtime::verify_bls(&key, &msg, &sig).is_ok(),\n"
+         "\t\t\t\tcess_gpu_verify_runtime::runtime::verify_bls_signature(&sig, &msg, &key).is_ok(),\n"
          "\t\t\t\tError::<T>::VerifyTeeSigFailed\n"
          "\t\t\t);\n"),
         ("\timpl<T: Config> Pallet<T> {\n\t\tfn clear_challenge(",

@@ -91,9 +91,47 @@ def parse():
 # ---------------------------------------------------------------------------
 # launcher + rendezvous (no GPU in this process)
 # ---------------------------------------------------------------------------
+def node_gpu_count():
+    """GPUs this job may use, counted WITHOUT a HIP call (the launcher parent
+    must not initialise the GPU): KFD topology nodes that have SIMDs, narrowed
+    by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.
+    CESS_BENCH_DEVICE_COUNT overrides it (the CPU test of the fail-fast path).
+    None when it cannot be told (no KFD topology: a CPU container)."""
+    o = os.environ.get("CESS_BENCH_DEVICE_COUNT")
+    if o is not None:
+        return int(o)
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for d in os.listdir(topo):
+            with open(os.path.join(topo, d, "properties")) as f:
+                props = dict(line.split() for line in f if len(line.split()) == 2)
+            n += int(props.get("simd_count", "0")) > 0
+    except OSError:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def fail(kind: str, code: int, **info):
+    """One JSON error line on stderr and a non-zero exit, before any rank has
+    a communicator (nothing to hang on, nothing to abort)."""
+    print(json.dumps(dict({"error": kind}, **info)), file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
 def launch(args) -> int:
     """Start args.gpus ranks with torch.distributed.run and return its exit code.
-    This parent process makes no HIP call (it only imports the launcher)."""
+    This parent process makes no HIP call (it only imports the launcher).  A
+    node with fewer visible GPUs than ranks fails here, before any rank starts
+    (each rank checks again under an external torchrun)."""
+    ndev = node_gpu_count()
+    if ndev is not None and ndev < args.gpus and not args.one_device and (
+            not args.dry_run or "CESS_BENCH_DEVICE_COUNT" in os.environ):
+        fail("devices", 4, need=args.gpus, visible=ndev, where="launcher")
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -140,9 +178,12 @@ def rdv_cleanup(rank: int, world: int):
         shutil.rmtree(rdv_dir(), ignore_errors=True)
 
 
-def comm_setup(ctx, rank: int, world: int, transport: str = "rccl"):
+def comm_setup(ctx, rank: int, world: int, transport: str = "rccl", one_device: bool = False) -> dict:
     """ncclUniqueId (or the shared-memory job name) from rank 0 to every rank
-    (file rendezvous), then the communicator inside the library."""
+    (file rendezvous), then the communicator inside the library.  Returns what
+    the communicator itself reports (cess_bls_comm_info: a collective, every
+    rank asks); under RCCL with one GPU per rank the job must span WORLD_SIZE
+    distinct devices, else every rank exits non-zero here, before any data."""
     from cess_amd import bls
     if transport == "shm":
         if rank == 0:
@@ -150,21 +191,32 @@ def comm_setup(ctx, rank: int, world: int, transport: str = "rccl"):
         ctx.comm_init_shm(world, rank, rdv_get("comm_name").decode())
         ctx.comm_barrier()
         rdv_cleanup(rank, world)
-        return
-    if rank == 0:
-        rdv_put("comm_id", bls.comm_id())
-    cid = rdv_get("comm_id")
-    try:
-        ctx.comm_init(world, rank, cid)
-        ctx.comm_barrier()
-    except bls.BlsInfraError as ex:
-        # a peer never arrived (CESS_BLS_COMM_TIMEOUT_MS) or RCCL failed: exit
-        # non-zero at once.  _exit, because a rank whose RCCL bootstrap never
-        # completed keeps a helper thread blocked inside RCCL (include/cess_bls.h)
-        print(json.dumps({"error": "communicator", "status": ex.status, "rank": rank, "message": str(ex)}),
-              file=sys.stderr, flush=True)
-        os._exit(3)
-    rdv_cleanup(rank, world)
+    else:
+        if rank == 0:
+            rdv_put("comm_id", bls.comm_id())
+        cid = rdv_get("comm_id")
+        try:
+            ctx.comm_init(world, rank, cid)
+            ctx.comm_barrier()
+        except bls.BlsInfraError as ex:
+            # a peer never arrived (CESS_BLS_COMM_TIMEOUT_MS) or RCCL failed: exit
+            # non-zero at once.  _exit, because a rank whose RCCL bootstrap never
+            # completed keeps a helper thread blocked inside RCCL (include/cess_bls.h)
+            print(json.dumps({"error": "communicator", "status": ex.status, "rank": rank, "message": str(ex)}),
+                  file=sys.stderr, flush=True)
+            os._exit(3)
+        rdv_cleanup(rank, world)
+    ci = ctx.comm_info()
+    info = {"kind": ctx.comm_kind, "nranks": ci["nranks"], "rank": ci["rank"], "bus_ids": ci["bus_ids"],
+            "distinct_devices": len(set(ci["bus_ids"]))}
+    if info["nranks"] != world or info["rank"] != rank:
+        print(json.dumps(dict(info, error="communicator shape", world=world)), file=sys.stderr, flush=True)
+        os._exit(5)
+    if transport == "rccl" and not one_device and info["distinct_devices"] != world:
+        # every rank saw the same gathered bus ids, so every rank exits here
+        print(json.dumps(dict(info, error="ranks share a device", world=world)), file=sys.stderr, flush=True)
+        os._exit(5)
+    return info
 
 
 def runtime_provenance() -> dict:
@@ -633,40 +685,57 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
+        if world > 1 and not args.one_device and "CESS_BENCH_DEVICE_COUNT" in os.environ:
+            ndev = int(os.environ["CESS_BENCH_DEVICE_COUNT"])
+            if ndev < world or local >= ndev:
+                fail("devices", 4, need=world, visible=ndev, rank=rank, where="rank")
         run_dry(args, rank, world)
         return
+    if world > 1:
+        # the communicator's init (and every wait on it) gives up after this
+        # deadline with CESS_BLS_E_COMM: a job with a missing peer ends in two
+        # minutes, well inside any driver time limit, instead of 300 s
+        os.environ.setdefault("CESS_BLS_COMM_TIMEOUT_MS", "120000")
 
     # the library (and with it /opt/rocm's HIP runtime and RCCL) first
     from cess_amd import bls
-    bls.load_library()
+    lib = bls.load_library()
     import numpy as np
+    if world > 1 and not args.one_device:
+        # one GPU per rank: fewer visible devices than ranks (or a local rank
+        # past them) fails every rank at once, before any context or
+        # communicator exists
+        ndev = int(os.environ.get("CESS_BENCH_DEVICE_COUNT", lib.cess_bls_device_count()))
+        if ndev < world or local >= ndev:
+            fail("devices", 4, need=world, visible=ndev, rank=rank, local_rank=local, where="rank")
 
     n = args.n or (N1_DEFAULT if world == 1 else NPER_MULTI)
     if args.mode == "rsa":
         ctx = bls.Context(device=local, max_batch=1 << 16, profile=True)
         if world > 1:
-            comm_setup(ctx, rank, world, args.transport)
+            comm_setup(ctx, rank, world, args.transport, args.one_device)
         run_rsa(args, ctx, rank, world)
         ctx.close()
         return
     if args.mode == "sign":
         ctx = bls.Context(device=local, max_batch=min(n, 1 << 20), profile=True)
         if world > 1:
-            comm_setup(ctx, rank, world, args.transport)
+            comm_setup(ctx, rank, world, args.transport, args.one_device)
         run_sign(args, ctx, rank, world)
         ctx.close()
         return
     if args.mode == "rlc":
         ctx = bls.Context(device=local, max_batch=min(args.n or (4 << 20), 1 << 20))
         if world > 1:
-            comm_setup(ctx, rank, world, args.transport)
+            comm_setup(ctx, rank, world, args.transport, args.one_device)
         run_rlc(args, ctx, rank, world)
         ctx.close()
         return
 
     ctx = bls.Context(device=local, max_batch=min(n, 1 << 20), profile=True)
+    comm = None
     if world > 1:
-        comm_setup(ctx, rank, world, args.transport)
+        comm = comm_setup(ctx, rank, world, args.transport, args.one_device)
     n_total = n * world
     keyed = args.mode == "keyed"
     if keyed:
@@ -715,6 +784,9 @@ def main():
     if world > 1:
         ctx.comm_barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = None
+    if world > 1:   # every rank's own step time (min / max over ranks)
+        rank_ms = {"min": -ctx.comm_max(-elapsed) / args.steps * 1e3, "max": ctx.comm_max(elapsed) / args.steps * 1e3}
     # per-launch HIP events on each kernel's own stream, timed region only
     stats = {k: v for k, v in ctx.stage_stats(reset=True).items() if v[1] > 0}
     if keyed:   # the keyed pipeline runs k_merge_pk in k_decode_pk's slot and has no per-signature prepare
@@ -732,13 +804,7 @@ def main():
     words = np.frombuffer(ctx.from_device(d_bitmap, world * wpr * 8), dtype=np.uint64)
     popcount = int(np.unpackbits(words.view(np.uint8)).sum())
     ok = local_ok if world == 1 else ctx.comm_max(0.0 if local_ok else 1.0) == 0.0
-    # what the communicator itself reports (collective: every rank asks)
-    comm = None
-    if world > 1:
-        ci = ctx.comm_info()
-        comm = {"kind": ctx.comm_kind, "nranks": ci["nranks"], "rank": ci["rank"], "bus_ids": ci["bus_ids"],
-                "distinct_devices": len(set(ci["bus_ids"]))}
-        assert ci["nranks"] == world, (ci, world)
+    # `comm`: what the communicator itself reported at setup (comm_setup)
 
     # the same records from HOST buffers (cess_bls_verify_batch: H2D copies,
     # the pipeline, D2H of codes + bitmap), as node callers pass them; reported
@@ -822,6 +888,7 @@ def main():
             "host_buffers_sigs_per_s": host_rate["sigs_per_s"] if host_rate else None,
             "host_buffers": host_rate,
             "comm": comm,
+            "rank_ms_per_step": rank_ms,
             "bitmap_popcount": popcount,
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "stage_launches_per_step": {k: v / args.steps for k, v in launches_of.items()},

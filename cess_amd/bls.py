@@ -37,7 +37,7 @@ EXPORTS = (
     "cess_bls_ctx_create", "cess_bls_ctx_destroy", "cess_bls_verify", "cess_bls_verify_batch",
     "cess_bls_verify_batch_var", "cess_bls_verify_batch_device", "cess_bls_public_key_batch",
     "cess_bls_sign_batch", "cess_bls_sign_batch_device", "cess_bls_hash_to_g1_batch", "cess_bls_gt_batch", "cess_bls_stage_times",
-    "cess_bls_status_string", "cess_bls_version",
+    "cess_bls_status_string", "cess_bls_version", "cess_bls_device_count",
     "cess_bls_verify_batch_rlc", "cess_bls_rlc_begin", "cess_bls_gt_product_is_one", "cess_bls_rlc_finish",
     "cess_bls_keys_load", "cess_bls_verify_batch_keyed", "cess_bls_verify_batch_keyed_device",
     "cess_bls_comm_id", "cess_bls_comm_init", "cess_bls_shard_range", "cess_bls_verify_batch_sharded",
@@ -173,6 +173,8 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_status_string.restype = ctypes.c_char_p
         lib.cess_bls_status_string.argtypes = [ctypes.c_int]
         lib.cess_bls_version.restype = ctypes.c_char_p
+        lib.cess_bls_device_count.restype = ctypes.c_int
+        lib.cess_bls_device_count.argtypes = []
         _lib = lib
         return lib
 

@@ -21,6 +21,7 @@
 // component ((w / 12) % 2) of fp2 (w / 24); rows of 4 words are uint4.
 #pragma once
 #include "pairing.hpp"
+#include "diag.hpp"
 
 namespace bls {
 
@@ -565,8 +566,8 @@ CESS_HD fp2 cyc_z0(const fp2& z1, const fp2& z2, const fp2& z3, const fp2& z4, c
 // denominators in the z0 words; safegcd inversion), then z0.  A lane whose
 // denominator vanishes (z2 = z3 = 0, e.g. a = 1 from an identity pair) redoes
 // its chain with Granger-Scott squarings (divergent, rare).
-template <class B, class XFn, class P>
-CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
+template <class B, class XFn, class P, class DG = NoDiag>
+CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk, DG* dg = nullptr) {
   {
     pk.st(0, base.ld(1));   // z4, z5 of the running power
     pk.st(1, base.ld(5));
@@ -575,7 +576,9 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
 #pragma unroll 1
     for (int j = 0; j < 6; j++) {
       const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+      if (dg) dg->template mark<0>();
       kcyc_run(pk, z2, z3, stop - k);
+      if (dg) dg->template mark<3>();   // compressed squarings
       k = stop;
       CESS_MEMBAR();
       const auto x = X(j);
@@ -625,6 +628,7 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
     }
     cyc_square_run(w, pk, 1);
   }
+  if (dg) dg->template mark<4>();   // decompression (and the rare fallback)
 }
 
 // Run the program.  The accumulator alternates between the stores acc0 and
@@ -634,8 +638,9 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk) {
 // the Miller-loop output on entry); `pk` is also the parking store of
 // cyc_square_run.  Returns the index (0/1) of the store holding the
 // result.
-template <class A, class SlotFn, class P>
-CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)[2], SlotFn&& slot, const P& pk) {
+template <class A, class SlotFn, class P, class DG = NoDiag>
+CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)[2], SlotFn&& slot, const P& pk,
+                             DG* dg = nullptr) {
   int cur = 0;
 #pragma unroll 1
   for (int pc = 0;; pc++) {
@@ -648,6 +653,7 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
       case FE_MUL:
         mul12_stream(cur ? acc0 : acc1, acc, slot(arg), pk);
         cur ^= 1;
+        if (dg) dg->template mark<1>();
         break;
       case FE_SQN: cyc_square_run(acc, pk, arg); break;
       case FE_CONJ: conj12(acc); break;
@@ -655,10 +661,12 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
       case FE_INV:   // into the other accumulator, like FE_MUL
         inv12_stream(cur ? acc0 : acc1, acc, pk);
         cur ^= 1;
+        if (dg) dg->template mark<2>();
         break;
-      case FE_CHAIN: cyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }, pk); break;
+      case FE_CHAIN: cyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }, pk, dg); break;
       default: break;
     }
+    if (dg) dg->template mark<0>();   // LOAD / STORE / SQN / CONJ / FROB (and the switch itself)
   }
   return cur;
 }
@@ -670,9 +678,11 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
 // pt(pair) yields the pair's affine G1 point; src(pair, step) its coefficients.
 // norm1: pair 1's lines are normalised to c2 = 1 as well (a distinct-key table
 // after normalize_lines); otherwise they take the general sparse product.
-template <class S, class Pt, class Src>
-CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1 = false) {
+template <class S, class Pt, class Src, class DG = NoDiag>
+CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1 = false,
+                                 DG* dg = nullptr) {
   set_one12(f);
+  if (dg) dg->template mark<5>();
 #pragma unroll 1
   for (int s = 0; s < N_COEFFS; s++) {
     // pair 1 (H(m), key) first: with pair 0 (sig, -G2) second k_miller's
@@ -685,16 +695,24 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
       coeff3 k = src(pr, s);
       g1a p = pt(pr);
       fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
+      if (dg) {
+        if (pr) dg->template mark<0>(); else dg->template mark<2>();
+      }
       if (pr && !norm1)
         mul014(f, k.c2, c1, c4);
       else
         mul014_one(f, c1, c4);   // -G2 table (and normalised key tables): c2 = 1
       CESS_MEMBAR();
+      if (dg) {
+        if (pr) dg->template mark<1>(); else dg->template mark<3>();
+      }
     }
     if (square_after_step(s)) sqr12(f);
     CESS_MEMBAR();
+    if (dg) dg->template mark<4>();
   }
   conj12(f);   // x < 0
+  if (dg) dg->template mark<5>();
 }
 
 }  // namespace bls

@@ -21,6 +21,11 @@ const char* kStageNames[ST_N] = {"k_decode_sig", "k_decode_pk",    "k_hash",    
 
 extern "C" const char* cess_bls_version(void) { return "cess_amd-bls 0.2 (gfx950)"; }
 
+extern "C" int cess_bls_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess && n > 0 ? n : 0;
+}
+
 extern "C" const char* cess_bls_status_string(int s) {
   switch (s) {
     case CESS_BLS_OK: return "ok";

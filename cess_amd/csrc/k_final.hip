@@ -20,6 +20,10 @@ __constant__ uint8_t kFeProgramVerify[][2] = {CESS_FE_PROGRAM_VERIFY};
 // slower: 245 vs 212 ms per 1 M, profiles/r02g_sweep.txt)
 #define CESS_LB_F12 __launch_bounds__(256, 2)
 
+#if defined(CESS_DIAG)
+CESS_DIAG_TABLE(k_final)
+#endif
+
 __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
                                     uint4* __restrict__ slots, uint64_t* __restrict__ bitmap,
                                     uint8_t* __restrict__ gt_out, uint64_t stride) {
@@ -43,9 +47,18 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
       // verdict is OK without the exponentiation, and the lane does not take
       // the Karabina fallback (z2 = z3 = 0 redoes every chain in Granger-Scott
       // form, for its whole wave).  (Gt bytes requested: the full program.)
+#if defined(CESS_DIAG)
+      // regions: 0 other opcodes, 1 FE_MUL, 2 FE_INV, 3 compressed squarings,
+      // 4 decompression, 5 verdict
+      Diag dg;
+      dg.begin();
+      Diag* dgp = &dg;
+#else
+      NoDiag* dgp = nullptr;
+#endif
       if (gt_out || !is_one12(slot(SL_F))) {
         const int which = final_exp_staged(acc0, acc1, gt_out ? kFeProgram : kFeProgramVerify, slot,
-                                           LdsF12{park, wave_first_thread()});
+                                           LdsF12{park, wave_first_thread()}, dgp);
         const GlobF12W acc = which ? acc1 : acc0;
         if (!(gt_out ? is_one12(acc) : is_conj12(acc, slot(SL_T4)))) c = CODE_PAIRING;
         if (gt_out) {   // optional Gt bytes for parity tests (576 B per signature)
@@ -60,6 +73,10 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
           }
         }
       }
+#if defined(CESS_DIAG)
+      dg.mark<5>();
+      dg.end(cess_diag_tab);
+#endif
       code[i] = c;
     }
   }

@@ -15,6 +15,10 @@ using namespace cess;
 // per 1 M) were removed from the product source.
 #define CESS_LB_F12 __launch_bounds__(256, 1)
 
+#if defined(CESS_DIAG)
+CESS_DIAG_TABLE(k_miller)
+#endif
+
 __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ code,
                                      const uint8_t* __restrict__ inf, const uint32_t* __restrict__ sig_aff,
                                      const uint32_t* __restrict__ h_aff, const uint32_t* __restrict__ neg_g2,
@@ -61,6 +65,17 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
   // (Per-signature rows are not normalised: k_norm_keys over every record
   // costs 22 ms per 1 M against 18 ms saved here, profiles/round3_k_sweep.txt.)
   const bool norm1 = cnorm && cnorm[cj];
+#if defined(CESS_DIAG)
+  // regions: 0/1 pair-1 loads / sparse product, 2/3 pair 0, 4 squaring,
+  // 5 prologue + epilogue
+  Diag dg;
+  dg.begin();
+  miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1, &dg);
+  copy12(GlobF12{fout, stride, i}, f);
+  dg.mark<5>();
+  dg.end(cess_diag_tab);
+#else
   miller_loop2_staged(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1);
   copy12(GlobF12{fout, stride, i}, f);
+#endif
 }

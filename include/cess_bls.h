@@ -407,6 +407,13 @@ uint64_t cess_bls_launch_records(cess_bls_ctx* ctx);
 
 const char* cess_bls_status_string(int status);
 const char* cess_bls_version(void);
+/* HIP devices visible to this process (hipGetDeviceCount; 0 when there is no
+ * device or the runtime fails).  Initialises the HIP runtime: a launcher that
+ * must not touch the GPU counts devices some other way.  bench.py's ranks call
+ * it before any context or communicator exists, so an N-rank job on a node
+ * with fewer than N devices exits at once instead of meeting a peer-less
+ * communicator (no reference counterpart: node-side launch plumbing). */
+int cess_bls_device_count(void);
 
 #ifdef __cplusplus
 }

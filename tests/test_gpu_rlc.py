@@ -53,30 +53,48 @@ def test_rlc_all_valid_single_check(ctx):
     assert words[:3000 // 64] == [(1 << 64) - 1] * (3000 // 64)
 
 
+def _fixed_len_cases(vectors):
+    return [c for c in vectors["cases"] if len(bytes.fromhex(c["sig"])) == 48 and len(bytes.fromhex(c["pk"])) == 96]
+
+
 def test_rlc_codes_equal_per_signature_path(ctx, vectors):
     """Forgeries, bad encodings and the golden adversarial cases spread over a
-    9,000-record batch: bisection must isolate them with exact codes."""
+    9,000-record batch: bisection must isolate them with exact codes.  The
+    expected codes come from the CONSTRUCTION (signed by the library's sign
+    kernel, pinned by the reference's sign KAT: 0; forged: 5; golden record:
+    its fixture code, src/lib.rs:243-246), not from another run of the
+    product; the per-signature path must agree as a second check."""
+    from oracle import bls_oracle
     sigs, pks, msgs = _few_key_batch(ctx, 9000, 7, 2)
     rng = random.Random(3)
     idx = rng.sample(range(9000), 12)
+    want = [0] * 9000
     # forged: valid signature over another message
     msgs[idx[0]] = rng.randbytes(32)
     msgs[idx[1]] = msgs[idx[1]][:31] + bytes([msgs[idx[1]][31] ^ 1])
     # signature of another record (valid point, wrong pairing)
     sigs[idx[2]] = sigs[idx[3]]
-    # malformed signature encodings
+    want[idx[0]] = want[idx[1]] = want[idx[2]] = 5
+    # malformed signature encodings: the compression flag clear is no
+    # compressed point (G1Affine::from_compressed fails, src/lib.rs:144 ->
+    # SIG_POINT); the identity is a valid encoding whose pairing check fails
     sigs[idx[4]] = bytes([sigs[idx[4]][0] & 0x7F]) + sigs[idx[4]][1:]          # compression bit clear
     sigs[idx[5]] = b"\xc0" + bytes(47)                                         # identity signature
+    with pytest.raises(bls_oracle.Invalid):
+        bls_oracle.g1_from_compressed(sigs[idx[4]])
+    want[idx[4]], want[idx[5]] = 2, 5
     # golden adversarial records (non-subgroup sig, off-curve key, x >= p, ...)
-    cases = [c for c in vectors["cases"] if len(bytes.fromhex(c["sig"])) == 48 and len(bytes.fromhex(c["pk"])) == 96]
+    cases = _fixed_len_cases(vectors)
     for j, c in zip(idx[6:], cases[:6]):
         sigs[j], msgs[j], pks[j] = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+        want[j] = c["code"]
+    assert sorted({c["code"] for c in cases[:6]}) == [0, 2, 4, 5]
     S, P, M, offs = _pack(sigs, pks, msgs)
-    expect, ewords = ctx.verify_fixed(S, P, M, offs)
     codes, words, st = ctx.verify_rlc(S, P, M, offs, seed=bytes(32))
-    assert codes == expect
-    assert words == ewords
-    assert expect.count(0) < 9000 - 3
+    assert list(codes) == want
+    assert words[:9000 // 64] == [sum(1 << b for b in range(64) if want[64 * w + b] == 0) for w in range(9000 // 64)]
+    expect, ewords = ctx.verify_fixed(S, P, M, offs)
+    assert codes == expect and words == ewords
     assert st["checks"] > 1 and st["leaves"] >= 1
 
 
@@ -121,12 +139,15 @@ def test_rlc_bucket_sums_equal_scalar_multiples(ctx, vectors, rlc_sums_path):
     if rlc_sums_path != "msm":
         pytest.skip("compares both paths itself")
     sigs, pks, msgs = _few_key_batch(ctx, 20000, 6, 7)
+    want = [0] * 20000
     msgs[777] = bytes(32)                                        # forgery
     sigs[1234] = b"\xc0" + bytes(47)                             # identity signature
-    sigs[4321] = bytes([sigs[4321][0] & 0x7F]) + sigs[4321][1:]  # malformed
-    cases = [c for c in vectors["cases"] if len(bytes.fromhex(c["sig"])) == 48 and len(bytes.fromhex(c["pk"])) == 96]
+    sigs[4321] = bytes([sigs[4321][0] & 0x7F]) + sigs[4321][1:]  # malformed (compression flag clear)
+    want[777], want[1234], want[4321] = 5, 5, 2
+    cases = _fixed_len_cases(vectors)
     for j, c in zip(range(5000, 20000, 2500), cases):
         sigs[j], msgs[j], pks[j] = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+        want[j] = c["code"]
     packed = _pack(sigs, pks, msgs)
     seed = bytes(range(100, 132))
     gts, codes, stats = {}, {}, {}
@@ -139,9 +160,11 @@ def test_rlc_bucket_sums_equal_scalar_multiples(ctx, vectors, rlc_sums_path):
     # every bisection check decides the same way on both paths (a wrong
     # sub-range sum would fail a check the other path passes)
     assert stats["1"] == stats["0"] and stats["1"]["checks"] > 1
+    # codes by construction (fixture codes for the golden records), then the
+    # per-signature path as a second check
+    assert list(codes["1"]) == list(codes["0"]) == want
     expect, _ = ctx.verify_fixed(*packed)
-    assert codes["1"] == codes["0"] == expect
-    assert expect[777] == 5 and expect[4321] != 0 and expect.count(0) < 20000 - 3
+    assert codes["1"] == expect
 
 
 def test_rlc_bucket_path_large_batch(ctx, rlc_sums_path):
@@ -162,21 +185,66 @@ def test_rlc_bucket_path_large_batch(ctx, rlc_sums_path):
     assert st["leaves"] == 1 and st["checks"] == 1 + 16 + 5, st
 
 
+def _msm_ok(covered, segs):
+    """host_rlc.cpp msm_ok() under the default selection (env unset)."""
+    return 0 < segs <= 1024 and covered >= 64 * segs
+
+
 def test_rlc_points_kept_scalar_multiple_fallback(ctx, rlc_sums_path):
     """Default selection with 141 segments for 9,000 records (< 64 records per
-    segment): the points are kept on the device but the check takes the
-    per-record multiples (computed from them); codes stay exact."""
+    segment): the batch's points are NOT kept (the first check already fails
+    msm_ok) and every check takes the per-chunk multiples; codes stay exact."""
     if rlc_sums_path != "msm":
         pytest.skip("one run suffices")
     del os.environ["CESS_BLS_RLC_MSM"]
+    assert not _msm_ok(9000, 140 + 1)
     sigs, pks, msgs = _few_key_batch(ctx, 9000, 140, 9)
     msgs[10] = bytes(32)
     msgs[8000] = bytes(32)
     packed = _pack(sigs, pks, msgs)
-    expect, _ = ctx.verify_fixed(*packed)
     codes, words, st = ctx.verify_rlc(*packed, seed=bytes(32))
-    assert codes == expect and codes[10] == 5 and codes[8000] == 5 and codes.count(0) == 8998
+    want = [0] * 9000
+    want[10] = want[8000] = 5
+    assert list(codes) == want
+    expect, _ = ctx.verify_fixed(*packed)
+    assert codes == expect
     assert st["distinct_keys"] == 140 and st["checks"] > 1
+
+
+def test_rlc_kept_points_scale_all_at_bisection(ctx, rlc_sums_path):
+    """the first check takes the buckets (so the batch's points are
+    kept on the device, batch-wide Xs/Xh arrays of stride n with R.d_code /
+    R.d_inf), but the first bisection level fails msm_ok, so rlc_scale_all
+    computes the per-record multiples from those kept arrays.  200 key groups
+    over 12,864 records: 12,864 >= 64 x 201 for the first check; the level
+    splits the batch into ceil(12,864 / 2,048) = 7 ranges (host_rlc.cpp
+    kRlcLeaf, kRlcFan), which meet the 200 groups in >= 200 + 6 terms, 213+
+    segments, which would need >= 13,632 covered records; its ranges are
+    leaves (<= 2,048 records), so the batch takes exactly 1 + 7 checks.
+    Codes by construction, the per-signature path and the never-kept path
+    (CESS_BLS_RLC_MSM=0) agree."""
+    if rlc_sums_path != "msm":
+        pytest.skip("compares both paths itself")
+    n, k = 12864, 200
+    fan = -(-n // 2048)
+    assert fan == 7 and _msm_ok(n, k + 1) and not _msm_ok(n, fan + k + fan - 1) and 8 * k <= n
+    sigs, pks, msgs = _few_key_batch(ctx, n, k, 13)
+    want = [0] * n
+    for j in (17, 4444, 12863):
+        msgs[j] = bytes(32)
+        want[j] = 5
+    sigs[2000] = b"\xc0" + bytes(47)
+    want[2000] = 5
+    packed = _pack(sigs, pks, msgs)
+    del os.environ["CESS_BLS_RLC_MSM"]
+    codes, words, st = ctx.verify_rlc(*packed, seed=bytes(range(7, 39)))
+    assert st["distinct_keys"] == k and st["checks"] == 1 + fan and st["leaves"] >= 1
+    assert list(codes) == want
+    expect, _ = ctx.verify_fixed(*packed)
+    assert codes == expect
+    os.environ["CESS_BLS_RLC_MSM"] = "0"
+    codes0, _, st0 = ctx.verify_rlc(*packed, seed=bytes(range(7, 39)))
+    assert codes0 == codes and st0 == st
 
 
 def test_rlc_repeated_records(ctx, rlc_sums_path):

@@ -132,3 +132,35 @@ def test_deserialize_equals_oracle(ctx, vectors):
     # the reference-API mirror now takes the decode-only path
     ok_pk = next(p for p, w in zip(pks, want_p) if w == 0)
     assert bls.PublicKey.deserialize(ok_pk).serialize() == ok_pk
+
+
+def _runtime_verify_bls_signature(code, reference_fallback):
+    """Python mirror of utils/cess-gpu-verify-runtime runtime::verify_bls_signature
+    (what the patched audit extrinsic calls): codes 0-5 are the reference's own
+    verdicts, only UNAVAILABLE runs the reference function in wasm."""
+    if code == bls.CODE_OK:
+        return True
+    if code in (1, 2, 3, 4, 5):
+        return False
+    return reference_fallback()
+
+
+@pytest.mark.gpu
+def test_cache_codes_are_verdicts_for_malformed_records(ctx, vectors):
+    """the audit wiring must not reach a panicking verifier.
+    cess_bls_cache_verify_var answers every malformed golden record (wrong
+    length, non-point, non-subgroup, off-curve, flag abuse) with its code 1-4
+    -- a verdict -- never CODE_UNAVAILABLE, so a GPU node decides it exactly as
+    the reference's total verify_bls_signature (src/lib.rs:243-247) does on a
+    wasm node, with no fallback at all."""
+    recs, expect = _golden_records(vectors)
+    c = bls.VerdictCache(1 << 16)
+    st, codes, stats = c.verify(recs, ctx=ctx)
+    assert st == 0 and codes == expect
+    assert bls.CODE_UNAVAILABLE not in codes
+    assert {1, 2, 3, 4} <= set(codes)          # every malformed kind is present
+    fallbacks = []
+    for code, want in zip(codes, expect):
+        ok = _runtime_verify_bls_signature(code, lambda: fallbacks.append(1) or True)
+        assert ok == (want == 0)
+    assert not fallbacks

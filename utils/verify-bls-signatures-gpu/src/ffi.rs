@@ -171,6 +171,7 @@ extern "C" {
     pub fn cess_bls_launch_records(ctx: *mut cess_bls_ctx) -> u64;
     pub fn cess_bls_status_string(status: c_int) -> *const c_char;
     pub fn cess_bls_version() -> *const c_char;
+    pub fn cess_bls_device_count() -> c_int;
 
     // include/cess_rsa.h: cp_enclave_verify::verify_rsa (primitives/enclave-verify/src/lib.rs:221-228)
     pub fn cess_rsa_parse_key(der: *const u8, len: usize, format: c_int, n_out: *mut u8, n_cap: usize,

@@ -250,6 +250,15 @@ CESS_HD uint64_t zero_after(uint64_t x) {
 }
 #endif
 
+// opaque(x): an empty NON-volatile asm on a partial column sum, so LLVM can
+// neither reassociate it back into the carried accumulator chain nor is it
+// pinned in program order (it moves with its operand)
+#if defined(CESS_HOSTEMU)
+CESS_HD void opaque(uint64_t&) {}
+#else
+CESS_HD void opaque(uint64_t& x) { asm("" : "+v"(x)); }
+#endif
+
 // --- 28-bit compute domain ---------------------------------------------------
 constexpr uint32_t M28 = 0x0fffffffu;
 
@@ -281,27 +290,48 @@ CESS_HD fp pack28(const uint32_t (&l)[14]) {
 }
 
 // Montgomery reduction tail shared by mul and sqr:
-//   columns k of the double-width product are accumulated by `col(k, acc)`;
-//   the result (< 2p) is left in 14 x 28-bit digits t.
+//   columns k of the double-width product are accumulated by
+//   `col(k, h, acc)`, which adds the column's products a_i b_j with i of
+//   parity h (h = -1: all of them); the result (< 2p) is left in 14 x 28-bit
+//   digits t.
+// CESS_MONT_SEP: each column's products go to two fresh partial sums (by the
+// parity of i; the known m * p terms continue the second), and only their
+// merge, m_k and the shift stay on the carried chain -- the wave then has
+// independent mads to issue while the chain's mul_lo / and / mad / shift
+// steps complete.  A lazy Fp2 product in a dependent loop: 7,476 -> 6,524
+// cycles at one wave per SIMD, 13,085 -> 12,700 at two
+// (profiles/round5_j_fp_probe.txt, mul_sep<2,noq>).
+#ifndef CESS_MONT_SEP
+#define CESS_MONT_SEP 0
+#endif
 template <class Col>
 CESS_HD void mont28_d(Col&& col, uint32_t (&t)[14]) {
   uint32_t m[14];
   uint64_t acc = 0;
 #pragma unroll
-  for (int k = 0; k < 14; k++) {
-    col(k, acc);
+  for (int k = 0; k < 27; k++) {
+#if CESS_MONT_SEP
+    uint64_t sa = 0, sb = 0;
+    col(k, 0, sa);
+    col(k, 1, sb);
 #pragma unroll
-    for (int i = 0; i < k; i++) mac(acc, m[i], c::P28[k - i]);
-    m[k] = ((uint32_t)acc * c::PINV28) & M28;
-    mac(acc, m[k], c::P28[0]);
-    acc >>= 28;
-  }
+    for (int i = k < 14 ? 0 : k - 13; i < (k < 14 ? k : 14); i++) mac(sb, m[i], c::P28[k - i]);
+    opaque(sa);
+    opaque(sb);
+    sa += sb;
+    opaque(sa);
+    acc += sa;
+#else
+    col(k, -1, acc);
 #pragma unroll
-  for (int k = 14; k < 27; k++) {
-    col(k, acc);
-#pragma unroll
-    for (int i = k - 13; i < 14; i++) mac(acc, m[i], c::P28[k - i]);
-    t[k - 14] = (uint32_t)acc & M28;
+    for (int i = k < 14 ? 0 : k - 13; i < (k < 14 ? k : 14); i++) mac(acc, m[i], c::P28[k - i]);
+#endif
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * c::PINV28) & M28;
+      mac(acc, m[k], c::P28[0]);
+    } else {
+      t[k - 14] = (uint32_t)acc & M28;
+    }
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;   // result < 2p < 2^382: fits
@@ -314,36 +344,51 @@ CESS_HD fp mont28(Col&& col) {
 }
 
 // Two Montgomery reductions side by side (lazy Fp2 product):
-//   `col(k, acc0, acc1)` adds column k of each combined double-width value.
+//   `col(k, h, acc0, acc1)` adds column k of each combined double-width
+//   value, products a_i b_j with i of parity h (h = -1: all); CESS_MONT_SEP
+//   as mont28_d.
 template <class Col>
 CESS_HD void mont28x2(Col&& col, fp& out0, fp& out1) {
   uint32_t m0[14], m1[14], t0[14], t1[14];
   uint64_t acc0 = 0, acc1 = 0;
 #pragma unroll
-  for (int k = 0; k < 14; k++) {
-    col(k, acc0, acc1);
+  for (int k = 0; k < 27; k++) {
+#if CESS_MONT_SEP
+    uint64_t s0a = 0, s1a = 0, s0b = 0, s1b = 0;
+    col(k, 0, s0a, s1a);
+    col(k, 1, s0b, s1b);
 #pragma unroll
-    for (int i = 0; i < k; i++) {
+    for (int i = k < 14 ? 0 : k - 13; i < (k < 14 ? k : 14); i++) {
+      mac(s0b, m0[i], c::P28[k - i]);
+      mac(s1b, m1[i], c::P28[k - i]);
+    }
+    opaque(s0a);
+    opaque(s1a);
+    opaque(s0b);
+    opaque(s1b);
+    s0a += s0b;
+    s1a += s1b;
+    opaque(s0a);
+    opaque(s1a);
+    acc0 += s0a;
+    acc1 += s1a;
+#else
+    col(k, -1, acc0, acc1);
+#pragma unroll
+    for (int i = k < 14 ? 0 : k - 13; i < (k < 14 ? k : 14); i++) {
       mac(acc0, m0[i], c::P28[k - i]);
       mac(acc1, m1[i], c::P28[k - i]);
     }
-    m0[k] = ((uint32_t)acc0 * c::PINV28) & M28;
-    m1[k] = ((uint32_t)acc1 * c::PINV28) & M28;
-    mac(acc0, m0[k], c::P28[0]);
-    mac(acc1, m1[k], c::P28[0]);
-    acc0 >>= 28;
-    acc1 >>= 28;
-  }
-#pragma unroll
-  for (int k = 14; k < 27; k++) {
-    col(k, acc0, acc1);
-#pragma unroll
-    for (int i = k - 13; i < 14; i++) {
-      mac(acc0, m0[i], c::P28[k - i]);
-      mac(acc1, m1[i], c::P28[k - i]);
+#endif
+    if (k < 14) {
+      m0[k] = ((uint32_t)acc0 * c::PINV28) & M28;
+      m1[k] = ((uint32_t)acc1 * c::PINV28) & M28;
+      mac(acc0, m0[k], c::P28[0]);
+      mac(acc1, m1[k], c::P28[0]);
+    } else {
+      t0[k - 14] = (uint32_t)acc0 & M28;
+      t1[k - 14] = (uint32_t)acc1 & M28;
     }
-    t0[k - 14] = (uint32_t)acc0 & M28;
-    t1[k - 14] = (uint32_t)acc1 & M28;
     acc0 >>= 28;
     acc1 >>= 28;
   }
@@ -351,6 +396,66 @@ CESS_HD void mont28x2(Col&& col, fp& out0, fp& out1) {
   t1[13] = (uint32_t)acc1;
   out0 = pack28(t0);
   out1 = pack28(t1);
+}
+
+// Four Montgomery reductions side by side (two independent lazy Fp2
+// products, mul2): four accumulation chains per column instead of two, so a
+// single wave per SIMD has independent work to issue while one chain's
+// reduction step (m = acc * p' -> m * p[0] -> shift) completes.
+template <class Col>
+CESS_HD void mont28x4(Col&& col, fp& out0, fp& out1, fp& out2, fp& out3) {
+  uint32_t m0[14], m1[14], m2[14], m3[14], t0[14], t1[14], t2[14], t3[14];
+  uint64_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    col(k, -1, acc0, acc1, acc2, acc3);
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      mac(acc0, m0[i], c::P28[k - i]);
+      mac(acc1, m1[i], c::P28[k - i]);
+      mac(acc2, m2[i], c::P28[k - i]);
+      mac(acc3, m3[i], c::P28[k - i]);
+    }
+    m0[k] = ((uint32_t)acc0 * c::PINV28) & M28;
+    m1[k] = ((uint32_t)acc1 * c::PINV28) & M28;
+    m2[k] = ((uint32_t)acc2 * c::PINV28) & M28;
+    m3[k] = ((uint32_t)acc3 * c::PINV28) & M28;
+    mac(acc0, m0[k], c::P28[0]);
+    mac(acc1, m1[k], c::P28[0]);
+    mac(acc2, m2[k], c::P28[0]);
+    mac(acc3, m3[k], c::P28[0]);
+    acc0 >>= 28;
+    acc1 >>= 28;
+    acc2 >>= 28;
+    acc3 >>= 28;
+  }
+#pragma unroll
+  for (int k = 14; k < 27; k++) {
+    col(k, -1, acc0, acc1, acc2, acc3);
+#pragma unroll
+    for (int i = k - 13; i < 14; i++) {
+      mac(acc0, m0[i], c::P28[k - i]);
+      mac(acc1, m1[i], c::P28[k - i]);
+      mac(acc2, m2[i], c::P28[k - i]);
+      mac(acc3, m3[i], c::P28[k - i]);
+    }
+    t0[k - 14] = (uint32_t)acc0 & M28;
+    t1[k - 14] = (uint32_t)acc1 & M28;
+    t2[k - 14] = (uint32_t)acc2 & M28;
+    t3[k - 14] = (uint32_t)acc3 & M28;
+    acc0 >>= 28;
+    acc1 >>= 28;
+    acc2 >>= 28;
+    acc3 >>= 28;
+  }
+  t0[13] = (uint32_t)acc0;
+  t1[13] = (uint32_t)acc1;
+  t2[13] = (uint32_t)acc2;
+  t3[13] = (uint32_t)acc3;
+  out0 = pack28(t0);
+  out1 = pack28(t1);
+  out2 = pack28(t2);
+  out3 = pack28(t3);
 }
 
 // a * b * 2^-392 mod p
@@ -362,10 +467,10 @@ CESS_HD fp mul(const fp& a0, const fp& b0) {
   uint32_t x[14], y[14];
   unpack28(a, x);
   unpack28(b, y);
-  fp r = mont28([&](int k, uint64_t& acc) {
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++)
-      if (k - i >= 0 && k - i < 14) mac(acc, x[i], y[k - i]);
+      if (k - i >= 0 && k - i < 14 && (h < 0 || (i & 1) == h)) mac(acc, x[i], y[k - i]);
   });
   seq(r);
   return r;
@@ -380,13 +485,13 @@ CESS_HD fp sqr(const fp& a0) {
   unpack28(a, x);
 #pragma unroll
   for (int i = 0; i < 14; i++) x2[i] = x[i] << 1;
-  fp r = mont28([&](int k, uint64_t& acc) {
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++) {
       const int j = k - i;
-      if (j > i && j < 14) mac(acc, x[i], x2[j]);
+      if (j > i && j < 14 && (h < 0 || (i & 1) == h)) mac(acc, x[i], x2[j]);
     }
-    if ((k & 1) == 0 && (k >> 1) < 14) mac(acc, x[k >> 1], x[k >> 1]);
+    if ((k & 1) == 0 && (k >> 1) < 14 && (h < 0 || ((k >> 1) & 1) == h)) mac(acc, x[k >> 1], x[k >> 1]);
   });
   seq(r);
   return r;
@@ -431,10 +536,10 @@ CESS_HD void mul_d(uint32_t (&r)[14], const uint32_t (&x)[14], const uint32_t (&
   CESS_COUNT_MUL();
   uint32_t t[14];
   mont28_d(
-      [&](int k, uint64_t& acc) {
+      [&](int k, int h, uint64_t& acc) {
 #pragma unroll
         for (int i = 0; i < 14; i++)
-          if (k - i >= 0 && k - i < 14) mac(acc, x[i], y[k - i]);
+          if (k - i >= 0 && k - i < 14 && (h < 0 || (i & 1) == h)) mac(acc, x[i], y[k - i]);
       },
       t);
 #pragma unroll
@@ -448,13 +553,13 @@ CESS_HD void sqr_d(uint32_t (&x)[14]) {
 #pragma unroll
   for (int i = 0; i < 14; i++) x2[i] = x[i] << 1;
   mont28_d(
-      [&](int k, uint64_t& acc) {
+      [&](int k, int h, uint64_t& acc) {
 #pragma unroll
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
-          if (j > i && j < 14) mac(acc, x[i], x2[j]);
+          if (j > i && j < 14 && (h < 0 || (i & 1) == h)) mac(acc, x[i], x2[j]);
         }
-        if ((k & 1) == 0 && (k >> 1) < 14) mac(acc, x[k >> 1], x[k >> 1]);
+        if ((k & 1) == 0 && (k >> 1) < 14 && (h < 0 || ((k >> 1) & 1) == h)) mac(acc, x[k >> 1], x[k >> 1]);
       },
       t);
 #pragma unroll
@@ -831,11 +936,11 @@ CESS_HD fp2 mul_scaled(const fp2& a, const fp2& b) {
   }
   fp2 r;
   mont28x2(
-      [&](int k, uint64_t& acc0, uint64_t& acc1) {
+      [&](int k, int h, uint64_t& acc0, uint64_t& acc1) {
 #pragma unroll
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
-          if (j < 0 || j >= 14) continue;
+          if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
           mac(acc0, x0[i], y0[j]);
           mac(acc1, x0[i], y1[j]);
           mac(acc0, x1[i], y1n[j]);
@@ -848,6 +953,69 @@ CESS_HD fp2 mul_scaled(const fp2& a, const fp2& b) {
   return r;
 }
 CESS_HD fp2 mul(const fp2& a, const fp2& b) { return mul_scaled<1>(a, b); }
+// Two independent lazy products r = S a b, q = S c d in ONE column loop
+// (mont28x4): the same mads and bounds as two mul_scaled<S> calls, but four
+// accumulation chains for the wave to interleave (a lone product measured
+// 4.9 cycles per instruction at one wave per SIMD against 4.0 for dot2's
+// denser columns, profiles/round5_e_fp_probe.txt).  For kernels with the
+// register room (working set ~260 VGPRs: k_miller).
+template <uint32_t S>
+CESS_HD void mul2_scaled(const fp2& a, const fp2& b, const fp2& c, const fp2& d, fp2& r, fp2& q) {
+  static_assert(S >= 1 && S <= 3, "digit bound");
+  CESS_COUNT_MUL2();
+  CESS_COUNT_MUL2();
+  fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1, c0 = c.c0, c1 = c.c1, d0 = d.c0, d1 = d.c1;
+  seq(a0);
+  seq(a1);
+  seq(b0);
+  seq(b1);
+  seq(c0);
+  seq(c1);
+  seq(d0);
+  seq(d1);
+  uint32_t x0[14], x1[14], y0[14], y1[14], y1n[14], u0[14], u1[14], w0[14], w1[14], w1n[14];
+  unpack28(a0, x0);
+  unpack28(a1, x1);
+  unpack28(b0, y0);
+  unpack28(b1, y1);
+  unpack28(c0, u0);
+  unpack28(c1, u1);
+  unpack28(d0, w0);
+  unpack28(d1, w1);
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    y1n[i] = c::NEG_K28[i] - y1[i];
+    w1n[i] = c::NEG_K28[i] - w1[i];
+    x0[i] *= S;
+    x1[i] *= S;
+    u0[i] *= S;
+    u1[i] *= S;
+  }
+  mont28x4(
+      [&](int k, int, uint64_t& acc0, uint64_t& acc1, uint64_t& acc2, uint64_t& acc3) {
+#pragma unroll
+        for (int i = 0; i < 14; i++) {
+          const int j = k - i;
+          if (j < 0 || j >= 14) continue;
+          mac(acc0, x0[i], y0[j]);
+          mac(acc1, x0[i], y1[j]);
+          mac(acc2, u0[i], w0[j]);
+          mac(acc3, u0[i], w1[j]);
+          mac(acc0, x1[i], y1n[j]);
+          mac(acc1, x1[i], y0[j]);
+          mac(acc2, u1[i], w1n[j]);
+          mac(acc3, u1[i], w0[j]);
+        }
+      },
+      r.c0, r.c1, q.c0, q.c1);
+  seq(r.c0);
+  seq(r.c1);
+  seq(q.c0);
+  seq(q.c1);
+}
+CESS_HD void mul2(const fp2& a, const fp2& b, const fp2& c, const fp2& d, fp2& r, fp2& q) {
+  mul2_scaled<1>(a, b, c, d, r, q);
+}
 #endif
 // a*b + c*d over Fp2 with ONE Montgomery reduction per output component:
 // the schoolbook form of mul(fp2, fp2) above, 8 half-products straight into
@@ -878,11 +1046,11 @@ CESS_HD fp2 dot2(const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
   for (int i = 0; i < 14; i++) yb1n[i] = c::NEG_K28[i] - yb1[i], yd1n[i] = c::NEG_K28[i] - yd1[i];
   fp2 r;
   mont28x2(
-      [&](int k, uint64_t& acc0, uint64_t& acc1) {
+      [&](int k, int h, uint64_t& acc0, uint64_t& acc1) {
 #pragma unroll
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
-          if (j < 0 || j >= 14) continue;
+          if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
           mac(acc0, xa0[i], yb0[j]);
           mac(acc1, xa0[i], yb1[j]);
           mac(acc0, xa1[i], yb1n[j]);
@@ -924,11 +1092,11 @@ CESS_HD fp2 sqr(const fp2& a) {
   }
   fp2 r;
   mont28x2(
-      [&](int k, uint64_t& acc0, uint64_t& acc1) {
+      [&](int k, int h, uint64_t& acc0, uint64_t& acc1) {
 #pragma unroll
         for (int i = 0; i < 14; i++) {
           const int j = k - i;
-          if (j < 0 || j >= 14) continue;
+          if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
           mac(acc0, s[i], d[j]);
           mac(acc1, x0[i], x1d[j]);
         }
@@ -1001,7 +1169,21 @@ CESS_HD fp6 mul_v(const fp6& a) { return {mul_nr(a.c2), a.c0, a.c1}; }
 // unreduced, for mul() operands only
 CESS_HD fp6 add_nr(const fp6& a, const fp6& b) { return {add_nr(a.c0, b.c0), add_nr(a.c1, b.c1), add_nr(a.c2, b.c2)}; }
 
+#ifndef CESS_MUL2
+#define CESS_MUL2 0
+#endif
 CESS_HD fp6 mul(const fp6& a, const fp6& b) {
+#if CESS_MUL2
+  // the six Karatsuba products as three independent pairs (mul2)
+  fp2 t0, t1, t2, u0, u1, u2;
+  mul2(a.c0, b.c0, a.c1, b.c1, t0, t1);
+  mul2(a.c2, b.c2, add_nr(a.c1, a.c2), add_nr(b.c1, b.c2), t2, u0);
+  mul2(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1), add_nr(a.c0, a.c2), add_nr(b.c0, b.c2), u1, u2);
+  fp2 c0 = add(mul_nr(sub(sub(u0, t1), t2)), t0);
+  fp2 c1 = add(sub(sub(u1, t0), t1), mul_nr(t2));
+  fp2 c2 = add(sub(sub(u2, t0), t2), t1);
+  return {c0, c1, c2};
+#else
   fp2 t0 = mul(a.c0, b.c0);
   fp2 t1 = mul(a.c1, b.c1);
   fp2 t2 = mul(a.c2, b.c2);
@@ -1010,6 +1192,7 @@ CESS_HD fp6 mul(const fp6& a, const fp6& b) {
   fp2 c1 = add(sub(sub(mul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1)), t0), t1), mul_nr(t2));
   fp2 c2 = add(sub(sub(mul(add_nr(a.c0, a.c2), add_nr(b.c0, b.c2)), t0), t2), t1);
   return {c0, c1, c2};
+#endif
 }
 CESS_HD fp6 sqr(const fp6& a) {
   // CH-SQR2
@@ -1036,7 +1219,13 @@ CESS_HD fp6 mul_by_01(const fp6& a, const fp2& b0, const fp2& b1) {
 }
 // a * (b1 v)
 CESS_HD fp6 mul_by_1(const fp6& a, const fp2& b1) {
+#if CESS_MUL2
+  fp2 p2, p0;
+  mul2(a.c2, b1, a.c0, b1, p2, p0);
+  return {mul_nr(p2), p0, mul(a.c1, b1)};
+#else
   return {mul_nr(mul(a.c2, b1)), mul(a.c0, b1), mul(a.c1, b1)};
+#endif
 }
 CESS_HD fp6 inv(const fp6& a) {
   fp2 c0 = sub(sqr(a.c0), mul_nr(mul(a.c1, a.c2)));

@@ -63,11 +63,11 @@ CESS_HD fp grp_mul_comp(const fp2& a, const fp2& b, uint32_t comp) {
     y0[i] = comp ? u1[i] : u0[i];
     y1[i] = comp ? u0[i] : c::NEG_K28[i] - u1[i];
   }
-  fp r = mont28([&](int k, uint64_t& acc) {
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++) {
       const int j = k - i;
-      if (j < 0 || j >= 14) continue;
+      if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
       mac(acc, x0[i], y0[j]);
       mac(acc, x1[i], y1[j]);
     }
@@ -89,10 +89,10 @@ CESS_HD fp grp_sqr_comp(const fp2& a, uint32_t comp) {
     xs[i] = comp ? x0[i] : x0[i] + x1[i];
     ys[i] = comp ? (x1[i] << 1) : x0[i] + (c::NEG_K28[i] - x1[i]);
   }
-  fp r = mont28([&](int k, uint64_t& acc) {
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++)
-      if (k - i >= 0 && k - i < 14) mac(acc, xs[i], ys[k - i]);
+      if (k - i >= 0 && k - i < 14 && (h < 0 || (i & 1) == h)) mac(acc, xs[i], ys[k - i]);
   });
   seq(r);
   return r;

@@ -180,9 +180,43 @@ CESS_HD bool is_conj12(const A& a, const B& b) {
   return r;
 }
 
+#ifndef CESS_SQR12_LOOP
+#define CESS_SQR12_LOOP 0
+#endif
+#ifndef CESS_MUL014_LOOP
+#define CESS_MUL014_LOOP 0
+#endif
 // f <- f^2  (complex squaring: 2 Fp6 multiplies)
 template <class S>
 CESS_HD void sqr12(const S& f) {
+#if CESS_SQR12_LOOP
+  // the two Fp6 products share ONE copy of the code (a two-pass loop over
+  // operands chosen per pass): half the instruction bytes of the squaring, so
+  // more of k_miller's step body stays in the instruction cache
+  fp6 ab;
+#pragma unroll 1
+  for (int it = 0; it < 2; it++) {
+    fp6 x, y;
+    {
+      const fp6 a0 = ld6(f, 0), a1 = ld6(f, 1);
+      if (it) {
+        x = add_nr(a0, a1);
+        y = add_nr(a0, mul_v(a1));
+      } else {
+        x = a0;
+        y = a1;
+      }
+    }
+    const fp6 r = mul(x, y);
+    CESS_MEMBAR();
+    if (it) {
+      st6(f, 0, sub(sub(r, ab), mul_v(ab)));
+      st6(f, 1, dbl(ab));
+    } else {
+      ab = r;
+    }
+  }
+#else
   fp6 ab;
   {
     fp6 a0 = ld6(f, 0), a1 = ld6(f, 1);
@@ -196,6 +230,7 @@ CESS_HD void sqr12(const S& f) {
   }
   st6(f, 0, sub(sub(x, ab), mul_v(ab)));
   st6(f, 1, dbl(ab));
+#endif
 }
 
 // a * (b0 + b1 v) for an Fp6 `a` in store half h (coefficients fetched per
@@ -218,6 +253,31 @@ CESS_HD fp6 mul_by_01_dot(const S& f, int h, const fp2& b0, const fp2& b1, const
 // f <- f * (c0 + c1 v + c4 v w)   (bls12_381 Fp12::mul_by_014, in place)
 template <class S>
 CESS_HD void mul014(const S& f, const fp2& c0, const fp2& c1, const fp2& c4) {
+#if CESS_MUL014_LOOP
+  // aa = f0 (c0 + c1 v) and t = (f0 + f1)(c0 + (c1 + c4) v) share one copy
+  // of mul_by_01_dot (a two-pass loop: half 0, then half 1 after f.c1 holds
+  // f0 + f1)
+  fp6 bb = mul_by_1(ld6(f, 1), c4);
+  CESS_MEMBAR();
+  fp6 aa;
+  const fp2 d = add(c1, c4);
+#pragma unroll 1
+  for (int it = 0; it < 2; it++) {
+    const fp2 b1 = it ? d : c1;
+    const fp6 r = mul_by_01_dot(f, it, c0, b1, mul_nr(b1));
+    CESS_MEMBAR();
+    if (it) {
+      st6(f, 1, sub(r, add(aa, bb)));
+    } else {
+      aa = r;
+      {
+        fp6 s = add(ld6(f, 0), ld6(f, 1));
+        st6(f, 1, s);                    // f.c1 <- a0 + a1 (consumed by pass 1)
+      }
+      st6(f, 0, add(mul_v(bb), aa));
+    }
+  }
+#else
   fp6 bb = mul_by_1(ld6(f, 1), c4);
   CESS_MEMBAR();
   fp6 aa = mul_by_01_dot(f, 0, c0, c1, mul_nr(c1));
@@ -232,17 +292,45 @@ CESS_HD void mul014(const S& f, const fp2& c0, const fp2& c1, const fp2& c4) {
   const fp2 d = add(c1, c4);
   fp6 t = mul_by_01_dot(f, 1, c0, d, mul_nr(d));
   st6(f, 1, sub(t, u));
+#endif
 }
 
 // a * (1 + b1 v): mul_by_01 with b0 = 1 (a reduced)
 CESS_HD fp6 mul_by_01_one(const fp6& a, const fp2& b1) {
+#if CESS_MUL2
+  fp2 p2, p0;
+  mul2(a.c2, b1, a.c0, b1, p2, p0);
+  return {add(a.c0, mul_nr(p2)), add(a.c1, p0), add(a.c2, mul(a.c1, b1))};
+#else
   return {add(a.c0, mul_nr(mul(a.c2, b1))), add(a.c1, mul(a.c0, b1)), add(a.c2, mul(a.c1, b1))};
+#endif
 }
 
 // f <- f * (1 + c1 v + c4 v w): mul014 for a line normalised to c0 = 1
 // (pairing.hpp normalize_line), 9 Fp2 products instead of 13
 template <class S>
 CESS_HD void mul014_one(const S& f, const fp2& c1, const fp2& c4) {
+#if CESS_MUL014_LOOP
+  fp6 bb = mul_by_1(ld6(f, 1), c4);
+  CESS_MEMBAR();
+  fp6 aa;
+  const fp2 d = add(c1, c4);
+#pragma unroll 1
+  for (int it = 0; it < 2; it++) {
+    const fp6 r = mul_by_01_one(ld6(f, it), it ? d : c1);
+    CESS_MEMBAR();
+    if (it) {
+      st6(f, 1, sub(r, add(aa, bb)));
+    } else {
+      aa = r;
+      {
+        fp6 s = add(ld6(f, 0), ld6(f, 1));
+        st6(f, 1, s);                    // f.c1 <- a0 + a1 (consumed by pass 1)
+      }
+      st6(f, 0, add(mul_v(bb), aa));
+    }
+  }
+#else
   fp6 bb = mul_by_1(ld6(f, 1), c4);
   CESS_MEMBAR();
   fp6 aa = mul_by_01_one(ld6(f, 0), c1);
@@ -256,6 +344,7 @@ CESS_HD void mul014_one(const S& f, const fp2& c1, const fp2& c4) {
   CESS_MEMBAR();
   fp6 t = mul_by_01_one(ld6(f, 1), add(c1, c4));
   st6(f, 1, sub(t, u));
+#endif
 }
 
 // f <- f * g  (Karatsuba over Fp6: 3 Fp6 multiplies)
@@ -512,8 +601,47 @@ CESS_HD void cyc_square_run(const A& acc, const P& pk, int n) {
 // half's two results stay in registers while the (z2, z3) half runs: the run
 // touches no HBM (k_final 171.3 -> 160.8 ms per 1 M against z4, z5 in the HBM
 // accumulator with the results parked in LDS, profiles/r02w_sweep.txt).
+#ifndef CESS_KCYC_LOOP
+#define CESS_KCYC_LOOP 0
+#endif
 template <class P>
 CESS_HD void kcyc_run(const P& pk, fp2& z2, fp2& z3, int n) {
+#if CESS_KCYC_LOOP
+  // the two halves share ONE copy of their products (b3 = 3 x y and
+  // t3 = 3 (x + y)(x + xi y)): a two-pass inner loop, (x, y) = (z4, z5) from
+  // the park, then (z2, z3); half the loop body's instruction bytes
+#pragma unroll 1
+  for (int r = 0; r < n; r++) {
+    fp2 u, v;
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+      CESS_MEMBAR();
+      fp2 x, y;
+      if (h) {
+        x = z2;
+        y = z3;
+      } else {
+        x = pk.ld(0);
+        y = pk.ld(1);
+      }
+      const fp2 b3 = mul_scaled<3>(x, y);
+      CESS_MEMBAR();
+      const fp2 t3 = mul_scaled<3>(add_nr(x, y), add_xi_nr(x, y));
+      const fp2 nb3 = mul_nr(b3);
+      const fp2 w = sub(sub(t3, b3), nb3);   // 3 (x^2 + xi y^2)
+      if (h) {
+        pk.st(0, sub(w, dbl(pk.ld(0))));
+        pk.st(1, dbl(add(pk.ld(1), b3)));
+      } else {
+        u = w;
+        v = dbl(nb3);   // 6 xi z4 z5
+      }
+    }
+    CESS_MEMBAR();
+    z2 = add(dbl(z2), v);
+    z3 = sub(u, dbl(z3));
+  }
+#else
 #pragma unroll 1
   for (int r = 0; r < n; r++) {
     CESS_MEMBAR();
@@ -538,6 +666,7 @@ CESS_HD void kcyc_run(const P& pk, fp2& z2, fp2& z3, int n) {
     z2 = add(dbl(z2), v);
     z3 = sub(u, dbl(z3));
   }
+#endif
 }
 
 // numerator / denominator of z1 of a compressed cyclotomic element:

@@ -14,6 +14,9 @@ using namespace cess;
 // LDS/HBM, HBM ping-pong with streamed operands: 314 / 244 / 203 vs 191 ms
 // per 1 M) were removed from the product source.
 #define CESS_LB_F12 __launch_bounds__(256, 1)
+#ifndef CESS_MILLER_UNIFORM01
+#define CESS_MILLER_UNIFORM01 0
+#endif
 
 #if defined(CESS_DIAG)
 CESS_DIAG_TABLE(k_miller)
@@ -58,7 +61,12 @@ __global__ CESS_LB_F12 void k_miller(uint64_t n, const uint8_t* __restrict__ cod
     return r;
   };
   auto src = [&](int pair, int k) {
+#if CESS_MILLER_UNIFORM01
+    // pair 0 takes mul014_one, which reads c0 and c1 only
+    return pair ? (cidx ? ld_coeff4(coeffs, cstride, cj, k) : ld_nt(k)) : ld_coeff_uniform01(neg_g2, k);
+#else
     return pair ? (cidx ? ld_coeff4(coeffs, cstride, cj, k) : ld_nt(k)) : ld_coeff_uniform(neg_g2, k);
+#endif
   };
   // cnorm (keyed batches): the key's lines were normalised to c2 = 1
   // (k_norm_keys), so pair 1 takes the 9-product sparse multiply as pair 0.

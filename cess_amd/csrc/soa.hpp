@@ -65,6 +65,21 @@ CESS_HD void st_coeff4_one(uint4* __restrict__ base, uint64_t stride, uint32_t i
     base[(uint64_t)(18 * k + 6 * j + q) * stride + i] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 // wave-uniform coefficient table (the -G2 constant): stride 1, same address in every lane
+// c0 and c1 of a line of a table normalised to c2 = 1 (the -G2 table after
+// k_norm_lines): 48 of the line's 72 dwords, so the 68 lines k_miller touches
+// per signature (13 KB) stay resident in the scalar data cache instead of
+// streaming 19.6 KB through it once per signature
+CESS_HD coeff3 ld_coeff_uniform01(const uint32_t* tab, int k) {
+  const uint32_t* b = tab + 72 * k;
+  coeff3 r;
+  fp* e = &r.c0.c0;
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+#pragma unroll
+    for (int l = 0; l < 12; l++) e[j].v[l] = b[12 * j + l];
+  r.c2 = fp2_one();
+  return r;
+}
 CESS_HD coeff3 ld_coeff_uniform(const uint32_t* tab, int k) {
   const uint32_t* b = tab + 72 * k;
   coeff3 r;

@@ -330,3 +330,37 @@ def test_g1_subgroup_check_jacobian(emu):
         want = 1 if o.g1_in_subgroup((x, y)) else 0
         assert emu.emu_g1_torsion_free(limbs(x), limbs(y), 0) == want, (x, y)
         assert emu.emu_g1_torsion_free(limbs(x), limbs(y), 1) == want, (x, y)
+
+
+VARIANT_FLAGS = ["-DCESS_SQR12_LOOP=1", "-DCESS_MUL014_LOOP=1", "-DCESS_KCYC_LOOP=1", "-DCESS_MONT_SEP=1", "-DCESS_MUL2=1"]
+
+
+@pytest.fixture(scope="module")
+def emu_loops():
+    """The host build of the same headers with the code-size loop forms of the
+    Fp12 operations (sqr12 / mul014 / mul014_one as two-pass loops, the
+    Karabina squaring's halves sharing one copy): staged.hpp CESS_*_LOOP."""
+    lib = os.path.join(HERE, "hostemu", "libemu_loops.so")
+    hdr_dir = os.path.join(HERE, "..", "cess_amd", "csrc", "bls")
+    newest = max(os.path.getmtime(os.path.join(hdr_dir, f)) for f in os.listdir(hdr_dir))
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(newest, os.path.getmtime(SRC)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-DCESS_HOSTEMU", *VARIANT_FLAGS, "-shared", "-fPIC", SRC,
+                               "-o", lib])
+    return ctypes.CDLL(lib)
+
+
+@pytest.mark.parametrize("norm_pk", [0, 1])
+def test_loop_forms_keep_codes_and_gt(emu_loops, vectors, norm_pk):
+    """The loop forms compute the same Miller loop and final exponentiation:
+    golden codes and Gt bytes, with per-signature and normalised key lines."""
+    old = emu_loops.emu_set_norm_pk(norm_pk)
+    try:
+        for c in vectors["cases"]:
+            s, m, k = bytes.fromhex(c["sig"]), bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"])
+            gt = (ctypes.c_uint8 * 576)()
+            code = emu_loops.emu_verify(s, m, len(m), k, gt)
+            assert code == c["code"], c["name"]
+            if "gt" in c:
+                assert bytes(gt).hex() == c["gt"], c["name"]
+    finally:
+        emu_loops.emu_set_norm_pk(old)

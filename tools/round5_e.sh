@@ -1,0 +1,4 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/bank_probe > gpurun_out/r5e_bank_probe.txt 2>&1; rc=$?; cat gpurun_out/r5e_bank_probe.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 ./tools/fp_probe > gpurun_out/r5e_fp_probe.txt 2>&1; rc=$?; cat gpurun_out/r5e_fp_probe.txt; exit $rc

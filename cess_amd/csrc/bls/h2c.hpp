@@ -91,6 +91,10 @@ CESS_HD uint32_t xmd_b0_byte(const uint8_t* msg, uint32_t len, uint32_t pos, uin
 }
 
 // expand_message_xmd(msg, DST, 128) -> 32 big-endian words (b1 || b2 || b3 || b4)
+// SELECT: write b_idx through uniform selects instead of out[8 (idx - 1) + j]
+// (a loop-variant index puts `out` in scratch; the selects keep it in VGPRs,
+// which only pays where the caller has the registers: hash_to_g1_parked)
+template <bool SELECT = false>
 CESS_HD void expand_message_xmd_128(const uint8_t* msg, uint32_t len, uint32_t (&out)[32]) {
   uint32_t b0[8];
 #pragma unroll
@@ -147,7 +151,12 @@ CESS_HD void expand_message_xmd_128(const uint8_t* msg, uint32_t len, uint32_t (
     sha256_compress(st, blk2);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      out[8 * (idx - 1) + j] = st[j];
+      if (SELECT) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) out[8 * q + j] = idx == q + 1 ? st[j] : out[8 * q + j];
+      } else {
+        out[8 * (idx - 1) + j] = st[j];
+      }
       prev[j] = st[j];
     }
   }
@@ -304,5 +313,64 @@ CESS_HD g1a hash_to_g1(const uint8_t* msg, uint32_t len) {
   const fp zi = inv(t.z);
   return clear_cofactor_g1(mul(t.x, zi), mul(t.y, zi));
 }
+
+#if !defined(CESS_HOSTEMU)
+// hash_to_g1 with the values that wait across an SSWU exponentiation parked
+// in LDS (k_hash, CESS_HASH_PARK): the second field element u1 while the
+// first is mapped, and the first image Q0 while the second is mapped -- 48
+// dwords that otherwise stay in VGPRs beside the window-4 power table and
+// make k_hash spill (76 VGPRs, 304 B/lane).  park: 48 rows x 256 lanes, row r
+// of lane t at park[r][t].
+CESS_HD void park_fp(uint32_t (*park)[256], int row, uint32_t t, const fp& a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) park[row + i][t] = a.v[i];
+}
+CESS_HD fp unpark_fp(uint32_t (*park)[256], int row, uint32_t t) {
+  fp a;
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.v[i] = park[row + i][t];
+  return a;
+}
+CESS_HD g1a hash_to_g1_parked(const uint8_t* msg, uint32_t len, uint32_t (*park)[256], uint32_t t) {
+  fp u0;
+  {
+    uint32_t uni[32];
+    expand_message_xmd_128<true>(msg, len, uni);
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = uni[16 + k];
+    park_fp(park, 36, t, fp_from_be64_words(w));
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = uni[k];
+    u0 = fp_from_be64_words(w);
+  }
+  {
+    fp xn, xd, y;
+    map_to_curve_sswu(u0, xn, xd, y);
+    park_fp(park, 0, t, xn);
+    park_fp(park, 12, t, mul(y, xd));
+    park_fp(park, 24, t, xd);
+  }
+  CESS_MEMBAR();
+  g1p s;
+  {
+    fp xn, xd, y;
+    map_to_curve_sswu(unpark_fp(park, 36, t), xn, xd, y);
+    const g1p q = {xn, mul(y, xd), xd};
+    CESS_MEMBAR();
+    const g1p q0 = {unpark_fp(park, 0, t), unpark_fp(park, 12, t), unpark_fp(park, 24, t)};
+    s = iso_curve_add(q0, q);
+  }
+  g1a r;
+  r.inf = true;
+  r.x = fp_zero();
+  r.y = fp_one();
+  if (is_zero(s.z)) return r;   // Q0 = -Q1: the sum is O', its image O
+  const g1p tt = iso_map_proj(s.x, s.y, s.z);
+  if (is_zero(tt.z)) return r;   // s in the isogeny's kernel: image O
+  const fp zi = inv(tt.z);
+  return clear_cofactor_g1(mul(tt.x, zi), mul(tt.y, zi));
+}
+#endif
 
 }  // namespace bls

@@ -7,6 +7,10 @@
 using namespace bls;
 using namespace cess;
 
+#ifndef CESS_HASH_PARK
+#define CESS_HASH_PARK 0
+#endif
+
 __global__ CESS_LB void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,
                                                const uint64_t* __restrict__ offs, const uint8_t* __restrict__ code,
                                                uint32_t* __restrict__ h_aff, uint64_t stride) {
@@ -18,7 +22,12 @@ __global__ CESS_LB void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,
   if (!code || code[i] == 0) {   // (no code array: the small-batch path hashes beside the decodes)
     uint64_t o = offs[i];
     uint32_t len = (uint32_t)(offs[i + 1] - o);
+#if CESS_HASH_PARK
+    __shared__ uint32_t park[48][256];   // 48 KiB per block
+    h = hash_to_g1_parked(msgs + o, len, park, threadIdx.x);
+#else
     h = hash_to_g1(msgs + o, len);
+#endif
   }
   st_fp(h_aff, stride, i, h.x);
   st_fp(h_aff + 12 * stride, stride, i, h.y);

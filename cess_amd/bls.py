@@ -173,8 +173,9 @@ def load_library(path: str = LIB_PATH):
         lib.cess_bls_status_string.restype = ctypes.c_char_p
         lib.cess_bls_status_string.argtypes = [ctypes.c_int]
         lib.cess_bls_version.restype = ctypes.c_char_p
-        lib.cess_bls_device_count.restype = ctypes.c_int
-        lib.cess_bls_device_count.argtypes = []
+        if hasattr(lib, "cess_bls_device_count"):   # (absent from pre-round-5 builds used in A/B sweeps)
+            lib.cess_bls_device_count.restype = ctypes.c_int
+            lib.cess_bls_device_count.argtypes = []
         _lib = lib
         return lib
 

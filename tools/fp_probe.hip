@@ -31,16 +31,13 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 
-// opaque(x): an empty NON-volatile asm, so LLVM can neither reassociate a
-// partial sum back into the accumulator chain nor is it pinned in program
-// order (it moves with its operand)
-__device__ __forceinline__ void opaque(uint64_t& x) { asm("" : "+v"(x)); }
+// (opaque(): bls/field.hpp)
 
 // Lazy Fp2 product with the column work separated from the reduction chain:
 // per column, the a*b products go to fresh partial sums (two per component,
 // by digit parity), the m*p terms already known to another fresh sum, and
 // only their merge, m_k and the shift are on the carried chain.
-template <int SPLIT, bool QSEP = true>
+template <int SPLIT, bool QSEP = true, bool QBAL = false>
 __device__ __forceinline__ fp2 mul_sep(const fp2& a, const fp2& b) {
   fp a0 = a.c0, a1 = a.c1, b0 = b.c0, b1 = b.c1;
   seq(a0); seq(a1); seq(b0); seq(b1);
@@ -72,6 +69,12 @@ __device__ __forceinline__ fp2 mul_sep(const fp2& a, const fp2& b) {
       for (int i = lo; i < hi; i++) {
         mac(q0, m0[i], c::P28[k - i]);
         mac(q1, m1[i], c::P28[k - i]);
+      }
+    } else if (QBAL) {   // the known m*p terms split over the chains by the parity of i
+#pragma unroll
+      for (int i = lo; i < hi; i++) {
+        mac(s0[i % SPLIT], m0[i], c::P28[k - i]);
+        mac(s1[i % SPLIT], m1[i], c::P28[k - i]);
       }
     } else {   // the known m*p terms continue the last a*b partial sum's chain
 #pragma unroll
@@ -137,8 +140,8 @@ __global__ __launch_bounds__(256) void k_fp(uint64_t* out, const uint32_t* in, i
     if (OP == 4) a = mul_sep<1>(a, b);            // column sums off the reduction chain
     if (OP == 5) a = mul_sep<2>(a, b);            // ... split by digit parity
     if (OP == 6) a = mul_sep<2, false>(a, b);     // ... m*p terms on the second a*b chain
-    if (OP == 7) a = mul_sep<3>(a, b);
-    if (OP == 8) a = mul_sep<4>(a, b);
+    if (OP == 7) a = mul_sep<2, false, true>(a, b);
+    if (OP == 8) a = mul_sep<3, false>(a, b);
   }
   __builtin_amdgcn_sched_barrier(0);
   const uint64_t t1 = stamp();
@@ -170,7 +173,7 @@ int main() {
   CHK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount, iters = 2048;
   const char* names[9] = {"mul(fp2,fp2)", "sub(add,dbl) fp2", "dot2", "mul2 (2 products)", "mul_sep<1>", "mul_sep<2>",
-                          "mul_sep<2,noq>", "mul_sep<3>", "mul_sep<4>"};
+                          "mul_sep<2,noq>", "mul_sep<2,bal>", "mul_sep<3,noq>"};
   void (*fns[9])(uint64_t*, const uint32_t*, int) = {k_fp<0>, k_fp<1>, k_fp<2>, k_fp<3>, k_fp<4>, k_fp<5>,
                                                       k_fp<6>, k_fp<7>, k_fp<8>};
   uint64_t* out;

@@ -35,7 +35,7 @@ enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
 // segment; a bucket of cnt entries is summed in chunks of msm_chunk(cnt)
 // entries (at least 64, at most 32 chunks), one work item per chunk
 #define CESS_MSM_SEG_BUCKETS 4096u
-#define CESS_MSM_MAX_SEGS 1024u   // segments of one bucket pass (bucket tables <= 4 M entries)
+#define CESS_MSM_MAX_SEGS 256u    // segments of one bucket pass (bucket tables <= 1 M entries, ~190 MB)
 // Segments of one bucket pass (kernel argument): parts (perm-position ranges;
 // their signatures) are segments 0 .. nparts - 1, terms (part x key group
 // ranges; their hashes) nparts + t.  pos == nullptr: the batch's first check

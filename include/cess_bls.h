@@ -192,9 +192,13 @@ int cess_bls_gt_batch(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const ui
  * (getrandom(2)).  Batches with more than one distinct key per 8 records gain
  * nothing from a combination and are verified per signature.
  * The sums of a check are formed by 8-bit-window buckets (Pippenger) when the
- * check has at most 1,024 segments and 64 records per segment, else from each
- * record's multiples; env CESS_BLS_RLC_MSM=0 forces the latter, =1 the buckets
- * whenever the tables fit (tests).  Both give the same group elements. */
+ * check has at most 256 segments (one segment per range of records and per
+ * key group met) and 64 records per segment, else from each record's
+ * multiples; env CESS_BLS_RLC_MSM=0 forces the latter, =1 the buckets whenever
+ * the tables fit (tests).  Both give the same group elements.  Memory bound of
+ * the bucket pass: 4,096 buckets x ~180 B per segment on the device (<= 190 MB
+ * at 256 segments, kept by the context for reuse) and three host vectors of
+ * 4 B per bucket (<= 12 MB) per check. */
 int cess_bls_verify_batch_rlc(cess_bls_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* pks,
                               const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* seed32,
                               uint8_t* codes_out, uint64_t* bitmap_out,
@@ -276,7 +280,11 @@ int cess_bls_verify_batch_var_sharded(cess_bls_ctx* ctx, size_t n, const uint8_t
  * enqueued on `stream` (NULL: the context's); the call returns after a final
  * status agreement that waits for the all-gathers, so a failure on any rank
  * (also one after the work was enqueued) is returned on EVERY rank, and the
- * failing rank's gathered codes are CESS_BLS_CODE_UNAVAILABLE (no verdict). */
+ * failing rank's gathered codes are CESS_BLS_CODE_UNAVAILABLE (no verdict).
+ * BLOCKING: the host thread waits for the all-gathers before returning (since
+ * round 4; before, the call only enqueued).  A caller that overlapped host
+ * work with this call, or pipelined several calls, must move the call to a
+ * thread of its own. */
 int cess_bls_verify_batch_sharded_device(cess_bls_ctx* ctx, size_t n_total, const uint8_t* d_sigs,
                                          const uint8_t* d_pks, const uint8_t* d_msgs,
                                          const uint64_t* d_msg_offsets, uint8_t* d_codes_all,

@@ -187,7 +187,7 @@ def test_rlc_bucket_path_large_batch(ctx, rlc_sums_path):
 
 def _msm_ok(covered, segs):
     """host_rlc.cpp msm_ok() under the default selection (env unset)."""
-    return 0 < segs <= 1024 and covered >= 64 * segs
+    return 0 < segs <= 256 and covered >= 64 * segs
 
 
 def test_rlc_points_kept_scalar_multiple_fallback(ctx, rlc_sums_path):

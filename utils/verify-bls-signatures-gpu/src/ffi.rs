@@ -110,6 +110,8 @@ extern "C" {
     pub fn cess_bls_verify_batch_sharded(ctx: *mut cess_bls_ctx, n: usize, sigs: *const u8, pks: *const u8,
                                          msgs: *const u8, msg_offsets: *const u64, codes_out: *mut u8,
                                          bitmap_out: *mut u64) -> c_int;
+    /// Collective and BLOCKING: returns after the final status agreement, which
+    /// waits for the verdict all-gathers on the host (include/cess_bls.h).
     pub fn cess_bls_verify_batch_sharded_device(ctx: *mut cess_bls_ctx, n_total: usize, d_sigs: *const u8,
                                                 d_pks: *const u8, d_msgs: *const u8, d_msg_offsets: *const u64,
                                                 d_codes_all: *mut u8, d_bitmap_all: *mut u64,

@@ -127,6 +127,9 @@ impl Default for Config {
 pub struct Verifier {
     ctx: *mut ffi::cess_bls_ctx,
     _devices: Vec<c_int>,
+    // rank count given to comm_init / comm_init_shm (0: no communicator): the
+    // C side writes that many bus ids in cess_bls_comm_info
+    comm_nranks: i32,
 }
 
 unsafe impl Send for Verifier {}
@@ -154,7 +157,7 @@ impl Verifier {
         };
         let mut p = core::ptr::null_mut();
         check(unsafe { ffi::cess_bls_ctx_create(&c, &mut p) })?;
-        Ok(Verifier { ctx: p, _devices: devices })
+        Ok(Verifier { ctx: p, _devices: devices, comm_nranks: 0 })
     }
 
     /// `verify_bls_signature(sig, msg, key)` (src/lib.rs:243-247) -> verdict code.
@@ -242,7 +245,9 @@ impl Verifier {
     }
     /// ncclCommInitRank on this context's GPU (collective).
     pub fn comm_init(&mut self, nranks: i32, rank: i32, id: &[u8; ffi::CESS_BLS_COMM_ID_BYTES]) -> Result<(), Error> {
-        check(unsafe { ffi::cess_bls_comm_init(self.ctx, nranks, rank, id.as_ptr()) })
+        check(unsafe { ffi::cess_bls_comm_init(self.ctx, nranks, rank, id.as_ptr()) })?;
+        self.comm_nranks = nranks;
+        Ok(())
     }
     /// Every rank passes the whole fixed-stride batch and gets all verdicts.
     pub fn verify_batch_sharded(&mut self, sigs: &[u8], pks: &[u8], msgs: &[u8], msg_offsets: &[u64])
@@ -273,11 +278,17 @@ impl Verifier {
         Ok(v)
     }
     /// What the communicator reports: (rank count, own rank, each rank's PCI
-    /// bus id in rank order).  Collective: call it on every rank.
+    /// bus id in rank order).  Collective: call it on every rank.  ONE call to
+    /// cess_bls_comm_info with the buffer sized from the rank count given at
+    /// init (what the C side writes), so a rank whose local query fails still
+    /// joins the collective and its peers never wait for it until the comm
+    /// deadline.
     pub fn comm_info(&mut self) -> Result<(i32, i32, Vec<String>), Error> {
+        if self.comm_nranks <= 0 {
+            return Err(Error::NoComm);
+        }
         let (mut nr, mut rk) = (0 as c_int, 0 as c_int);
-        check(unsafe { ffi::cess_bls_comm_info(self.ctx, &mut nr, &mut rk, core::ptr::null_mut()) })?;
-        let mut buf = vec![0 as core::ffi::c_char; nr.max(1) as usize * ffi::CESS_BLS_BUS_ID_BYTES];
+        let mut buf = vec![0 as core::ffi::c_char; self.comm_nranks as usize * ffi::CESS_BLS_BUS_ID_BYTES];
         check(unsafe { ffi::cess_bls_comm_info(self.ctx, &mut nr, &mut rk, buf.as_mut_ptr()) })?;
         let ids = buf
             .chunks(ffi::CESS_BLS_BUS_ID_BYTES)
@@ -288,7 +299,9 @@ impl Verifier {
     /// Host shared-memory transport instead of RCCL (ranks on one host, which
     /// may share a GPU); `name` from `Verifier::comm_shm_name` on one rank.
     pub fn comm_init_shm(&mut self, nranks: i32, rank: i32, name: &CStr) -> Result<(), Error> {
-        check(unsafe { ffi::cess_bls_comm_init_shm(self.ctx, nranks, rank, name.as_ptr()) })
+        check(unsafe { ffi::cess_bls_comm_init_shm(self.ctx, nranks, rank, name.as_ptr()) })?;
+        self.comm_nranks = nranks;
+        Ok(())
     }
     pub fn comm_shm_name() -> Result<std::ffi::CString, Error> {
         let mut buf = [0 as core::ffi::c_char; ffi::CESS_BLS_COMM_NAME_BYTES];

@@ -7,8 +7,11 @@
 using namespace bls;
 using namespace cess;
 
+// CESS_HASH_PARK: the SSWU's waiting values parked in LDS (bls/h2c.hpp
+// hash_to_g1_parked): 304 -> 24 B/lane scratch at equal time
+// (profiles/round5_k_sweep.txt: 25.32 vs 25.27 ms per 1 M)
 #ifndef CESS_HASH_PARK
-#define CESS_HASH_PARK 0
+#define CESS_HASH_PARK 1
 #endif
 
 __global__ CESS_LB void k_hash(uint64_t n, const uint8_t* __restrict__ msgs,

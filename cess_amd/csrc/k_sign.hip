@@ -43,7 +43,8 @@ __global__ CESS_LB void k_sign(uint64_t n, const uint8_t* __restrict__ sks, cons
   uint32_t k[8];
   load_sk(sks + 32 * i, k);
   uint64_t o = offs[i];
-  g1a h = hash_to_g1(msgs + o, (uint32_t)(offs[i + 1] - o));
+  __shared__ uint32_t park[48][256];   // SSWU values parked in LDS (k_hash.hip)
+  g1a h = hash_to_g1_parked(msgs + o, (uint32_t)(offs[i + 1] - o), park, threadIdx.x);
   g1a s;
   if (h.inf) {
     s = h;
@@ -60,7 +61,8 @@ __global__ CESS_LB void k_hash_out(uint64_t n, const uint8_t* __restrict__ msgs,
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t o = offs[i];
-  g1a h = hash_to_g1(msgs + o, (uint32_t)(offs[i + 1] - o));
+  __shared__ uint32_t park[48][256];
+  g1a h = hash_to_g1_parked(msgs + o, (uint32_t)(offs[i + 1] - o), park, threadIdx.x);
   uint8_t b[48];
   g1_compress(h, b);
   store_bytes(out + 48 * i, b, 48);

@@ -367,14 +367,32 @@ CESS_HD void mul12(const S& f, const G& g) {
 // fp6) keeps both 72-dword operands live as well, which spills at two waves
 // per SIMD.  Loaders may return unreduced sums (< 4p); sums of two of them
 // (< 8p) still satisfy mul()'s input bound.
+// CESS_FE_PF (measurement variant): the next diagonal product's operands are
+// loaded before the current product, so their HBM latency overlaps its mads
+// (48 more live VGPRs).
+#ifndef CESS_FE_PF
+#define CESS_FE_PF 0
+#endif
 template <class LA, class LB, class SK>
 CESS_HD void mul6_stream(LA&& a, LB&& b, SK&& sink) {
+#if CESS_FE_PF
+  fp2 pa = a(0), pb = b(0);
+  fp2 qa = a(1), qb = b(1);
+  const fp2 v0 = mul(pa, pb);
+  CESS_MEMBAR();
+  pa = a(2), pb = b(2);
+  const fp2 v1 = mul(qa, qb);
+  CESS_MEMBAR();
+  const fp2 v2 = mul(pa, pb);
+  CESS_MEMBAR();
+#else
   const fp2 v0 = mul(a(0), b(0));
   CESS_MEMBAR();
   const fp2 v1 = mul(a(1), b(1));
   CESS_MEMBAR();
   const fp2 v2 = mul(a(2), b(2));
   CESS_MEMBAR();
+#endif
   sink(0, add(mul_nr(sub(sub(mul(add_nr(a(1), a(2)), add_nr(b(1), b(2))), v1), v2)), v0));
   CESS_MEMBAR();
   sink(1, add(sub(sub(mul(add_nr(a(0), a(1)), add_nr(b(0), b(1))), v0), v1), mul_nr(v2)));
@@ -401,6 +419,42 @@ CESS_HD void mul12_stream(const D& d, const S& f, const G& g, const T& t) {
   CESS_MEMBAR();
   mul6_stream([&](int j) { return add_nr(f.ld(j), f.ld(3 + j)); },
               [&](int j) { return add_nr(g.ld(j), g.ld(3 + j)); },
+              [&](int j, const fp2& x) { d.st(3 + j, sub(sub(x, t.ld(j)), d.ld(3 + j))); });
+}
+
+// mul12_stream with the park `pk` (3 Fp2, LDS) caching each Fp6 product's
+// FIRST operand (f0, f1, then f0 + f1) instead of holding the temporary t0
+// (now the store `t`, an HBM slot): every a(j) of mul6_stream is an LDS read,
+// so f is read from HBM 12 times (Fp2) per product instead of 36 -- 60 Fp2
+// loads + 12 stores against 78 + 9 (k_final's HBM traffic is its clock:
+// the same instruction stream with L2-resident slots runs 2.36 instead of
+// 2.13 GHz, profiles/round5_v_diag_l2.txt).
+#ifndef CESS_FE_APARK
+#define CESS_FE_APARK 1
+#endif
+template <class D, class S, class G, class T, class P>
+CESS_HD void mul12_stream_ap(const D& d, const S& f, const G& g, const T& t, const P& pk) {
+#pragma unroll 1
+  for (int j = 0; j < 3; j++) pk.st(j, f.ld(j));
+  CESS_MEMBAR();
+  mul6_stream([&](int j) { return pk.ld(j); }, [&](int j) { return g.ld(j); },
+              [&](int j, const fp2& v) { t.st(j, v); });
+  CESS_MEMBAR();
+#pragma unroll 1
+  for (int j = 0; j < 3; j++) pk.st(j, f.ld(3 + j));
+  CESS_MEMBAR();
+  mul6_stream([&](int j) { return pk.ld(j); }, [&](int j) { return g.ld(3 + j); },
+              [&](int j, const fp2& v) { d.st(3 + j, v); });
+  d.st(0, add(t.ld(0), mul_nr(d.ld(5))));
+  d.st(1, add(t.ld(1), d.ld(3)));
+  d.st(2, add(t.ld(2), d.ld(4)));
+  CESS_MEMBAR();
+  // unreduced sums (< 4p) in the park: mul6_stream's own sums of two of them
+  // stay below 8p, mul()'s input bound (as in mul12_stream)
+#pragma unroll 1
+  for (int j = 0; j < 3; j++) pk.st(j, add_nr(f.ld(j), f.ld(3 + j)));
+  CESS_MEMBAR();
+  mul6_stream([&](int j) { return pk.ld(j); }, [&](int j) { return add_nr(g.ld(j), g.ld(3 + j)); },
               [&](int j, const fp2& x) { d.st(3 + j, sub(sub(x, t.ld(j)), d.ld(3 + j))); });
 }
 
@@ -494,8 +548,10 @@ CESS_HD void inv12_stream(const D& d, const S& f, const T& t) {
 // x are spelled out as square runs and multiplies by the base.
 // ---------------------------------------------------------------------------
 enum FeOp : uint8_t { FE_LOAD, FE_STORE, FE_MUL, FE_SQN, FE_CONJ, FE_FROB, FE_INV, FE_CHAIN, FE_END };
+// SL_TM: FE_MUL's Fp6 temporary when the park caches its first operand
+// (CESS_FE_APARK)
 enum FeSlot : uint8_t { SL_F = 0, SL_M, SL_T0, SL_T1, SL_T3, SL_T4, SL_T5, SL_T6,
-                        SL_X0, SL_X1, SL_X2, SL_X3, SL_X4, SL_X5, SL_N };
+                        SL_X0, SL_X1, SL_X2, SL_X3, SL_X4, SL_X5, SL_TM, SL_N };
 
 // a^x (x = -0xd201000000010000) for a in slot s: |x| has bits 63, 62, 60, 57,
 // 48, 16, so a^|x| = a^(2^63) a^(2^62) a^(2^60) a^(2^57) a^(2^48) a^(2^16).
@@ -780,7 +836,11 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
       case FE_LOAD: copy12(acc, slot(arg)); break;
       case FE_STORE: copy12(slot(arg), acc); break;
       case FE_MUL:
+#if CESS_FE_APARK
+        mul12_stream_ap(cur ? acc0 : acc1, acc, slot(arg), slot(SL_TM), pk);
+#else
         mul12_stream(cur ? acc0 : acc1, acc, slot(arg), pk);
+#endif
         cur ^= 1;
         if (dg) dg->template mark<1>();
         break;

@@ -35,7 +35,14 @@ __global__ CESS_LB_F12 void k_final(uint64_t n, uint8_t* __restrict__ code, uint
       // two HBM accumulators (slots SL_N - 1 and SL_N): FE_MUL ping-pongs.
       // Slot views start at the wave's first record (uniform) and add the
       // lane id per access (staged.hpp GlobF12W).
+#if defined(CESS_FE_L2PROBE)
+      // TIMING PROBE ONLY (wrong verdicts): every block's slot views alias the
+      // first block's records, so the slots' working set (~2.4 MB) stays in
+      // L2 -- k_final with its HBM latency removed
+      const uint32_t w0 = wave_first_thread();
+#else
       const uint32_t w0 = blockIdx.x * blockDim.x + wave_first_thread();
+#endif
       GlobF12W acc0{slots + (uint64_t)(SL_N - 1) * 36 * stride + w0, stride};
       GlobF12W acc1{slots + (uint64_t)SL_N * 36 * stride + w0, stride};
       // 18 uint4 rows x 256 lanes = 72 KiB per block: two blocks per CU

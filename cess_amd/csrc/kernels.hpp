@@ -28,8 +28,9 @@ enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
 #define CESS_W_G2 48u          // affine G2
 #define CESS_W_COEFFS 4896u    // 68 x 3 Fp2
 #define CESS_W_FP12 144u
-#define CESS_FE_SLOTS 15u      // HBM Fp12 slots of the final-exponentiation program (bls/staged.hpp):
-                               // 7 temporaries, 6 powers of FE_CHAIN, 2 ping-pong accumulators
+#define CESS_FE_SLOTS 16u      // HBM Fp12 slots of the final-exponentiation program (bls/staged.hpp):
+                               // 7 temporaries, 6 powers of FE_CHAIN, FE_MUL's Fp6 temporary (SL_TM),
+                               // 2 ping-pong accumulators
 
 // RLC bucket sums (k_rlc.hip k_msm_*): 16 windows x 256 digit buckets per
 // segment; a bucket of cnt entries is summed in chunks of msm_chunk(cnt)

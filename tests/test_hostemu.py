@@ -332,7 +332,7 @@ def test_g1_subgroup_check_jacobian(emu):
         assert emu.emu_g1_torsion_free(limbs(x), limbs(y), 1) == want, (x, y)
 
 
-VARIANT_FLAGS = ["-DCESS_SQR12_LOOP=1", "-DCESS_MUL014_LOOP=1", "-DCESS_KCYC_LOOP=1", "-DCESS_MONT_SEP=1", "-DCESS_MUL2=1"]
+VARIANT_FLAGS = ["-DCESS_SQR12_LOOP=1", "-DCESS_MUL014_LOOP=1", "-DCESS_KCYC_LOOP=1", "-DCESS_MONT_SEP=1", "-DCESS_MUL2=1", "-DCESS_FE_APARK=1"]
 
 
 @pytest.fixture(scope="module")

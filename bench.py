@@ -161,7 +161,11 @@ def rdv_put(name: str, data: bytes):
     os.replace(tmp, os.path.join(d, name))
 
 
-def rdv_get(name: str, timeout: float = 300.0) -> bytes:
+def rdv_get(name: str, timeout: float = None) -> bytes:
+    """Wait for rank 0's file; bounded by the same deadline as the
+    communicator (CESS_BLS_COMM_TIMEOUT_MS, 120 s by default for N > 1)."""
+    if timeout is None:
+        timeout = float(os.environ.get("CESS_BLS_COMM_TIMEOUT_MS", "120000")) / 1000.0
     p = os.path.join(rdv_dir(), name)
     t0 = time.time()
     while not os.path.exists(p):

@@ -262,6 +262,26 @@ CESS_HD void opaque(uint64_t& x) { asm("" : "+v"(x)); }
 // --- 28-bit compute domain ---------------------------------------------------
 constexpr uint32_t M28 = 0x0fffffffu;
 
+// The digit mask as an operand: a literal makes every v_and_b32 an 8-byte
+// instruction; held in an SGPR (CESS_M28_SGPR, a CSE-able non-volatile asm)
+// the AND is the 4-byte VOP2 form (one wave issues 4-byte instructions every
+// 4.04 cycles against 4.53 for 8-byte ones, profiles/round5_o_lat_probe.txt).
+// Measured, not adopted: k_miller +1.7-2.1 ms, k_final +1 ms (+788
+// instructions in k_miller's step; profiles/round5_aa_sweep.txt).
+#ifndef CESS_M28_SGPR
+#define CESS_M28_SGPR 0
+#endif
+#if CESS_M28_SGPR && !defined(CESS_HOSTEMU)
+CESS_HD uint32_t m28_sgpr() {
+  uint32_t m;
+  asm("s_mov_b32 %0, 0xfffffff" : "=s"(m));
+  return m;
+}
+#define M28V m28_sgpr()
+#else
+#define M28V M28
+#endif
+
 // acc += x * y (one v_mad_u64_u32; column sums stay below 2^64)
 CESS_HD void mac(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
 
@@ -272,7 +292,7 @@ CESS_HD void unpack28(const fp& a, uint32_t (&l)[14]) {
     const int off = 28 * k, i = off >> 5, sh = off & 31;
     uint32_t lo = a.v[i] >> sh;
     if (sh > 4 && i + 1 < 12) lo |= a.v[i + 1] << (32 - sh);
-    l[k] = lo & M28;
+    l[k] = lo & M28V;
   }
 }
 // 14 x 28-bit normalised limbs (value < 2^384) -> 12 x 32
@@ -327,10 +347,10 @@ CESS_HD void mont28_d(Col&& col, uint32_t (&t)[14]) {
     for (int i = k < 14 ? 0 : k - 13; i < (k < 14 ? k : 14); i++) mac(acc, m[i], c::P28[k - i]);
 #endif
     if (k < 14) {
-      m[k] = ((uint32_t)acc * c::PINV28) & M28;
+      m[k] = ((uint32_t)acc * c::PINV28) & M28V;
       mac(acc, m[k], c::P28[0]);
     } else {
-      t[k - 14] = (uint32_t)acc & M28;
+      t[k - 14] = (uint32_t)acc & M28V;
     }
     acc >>= 28;
   }
@@ -381,13 +401,13 @@ CESS_HD void mont28x2(Col&& col, fp& out0, fp& out1) {
     }
 #endif
     if (k < 14) {
-      m0[k] = ((uint32_t)acc0 * c::PINV28) & M28;
-      m1[k] = ((uint32_t)acc1 * c::PINV28) & M28;
+      m0[k] = ((uint32_t)acc0 * c::PINV28) & M28V;
+      m1[k] = ((uint32_t)acc1 * c::PINV28) & M28V;
       mac(acc0, m0[k], c::P28[0]);
       mac(acc1, m1[k], c::P28[0]);
     } else {
-      t0[k - 14] = (uint32_t)acc0 & M28;
-      t1[k - 14] = (uint32_t)acc1 & M28;
+      t0[k - 14] = (uint32_t)acc0 & M28V;
+      t1[k - 14] = (uint32_t)acc1 & M28V;
     }
     acc0 >>= 28;
     acc1 >>= 28;
@@ -416,10 +436,10 @@ CESS_HD void mont28x4(Col&& col, fp& out0, fp& out1, fp& out2, fp& out3) {
       mac(acc2, m2[i], c::P28[k - i]);
       mac(acc3, m3[i], c::P28[k - i]);
     }
-    m0[k] = ((uint32_t)acc0 * c::PINV28) & M28;
-    m1[k] = ((uint32_t)acc1 * c::PINV28) & M28;
-    m2[k] = ((uint32_t)acc2 * c::PINV28) & M28;
-    m3[k] = ((uint32_t)acc3 * c::PINV28) & M28;
+    m0[k] = ((uint32_t)acc0 * c::PINV28) & M28V;
+    m1[k] = ((uint32_t)acc1 * c::PINV28) & M28V;
+    m2[k] = ((uint32_t)acc2 * c::PINV28) & M28V;
+    m3[k] = ((uint32_t)acc3 * c::PINV28) & M28V;
     mac(acc0, m0[k], c::P28[0]);
     mac(acc1, m1[k], c::P28[0]);
     mac(acc2, m2[k], c::P28[0]);
@@ -439,10 +459,10 @@ CESS_HD void mont28x4(Col&& col, fp& out0, fp& out1, fp& out2, fp& out3) {
       mac(acc2, m2[i], c::P28[k - i]);
       mac(acc3, m3[i], c::P28[k - i]);
     }
-    t0[k - 14] = (uint32_t)acc0 & M28;
-    t1[k - 14] = (uint32_t)acc1 & M28;
-    t2[k - 14] = (uint32_t)acc2 & M28;
-    t3[k - 14] = (uint32_t)acc3 & M28;
+    t0[k - 14] = (uint32_t)acc0 & M28V;
+    t1[k - 14] = (uint32_t)acc1 & M28V;
+    t2[k - 14] = (uint32_t)acc2 & M28V;
+    t3[k - 14] = (uint32_t)acc3 & M28V;
     acc0 >>= 28;
     acc1 >>= 28;
     acc2 >>= 28;

@@ -65,7 +65,7 @@ E_INVALID_ARG, E_NO_DEVICE, E_HIP, E_OOM, E_RCCL, E_BUSY, E_BAD_KEY, E_BAD_SIG, 
 E_COMM = -11
 KIND_SIG, KIND_PK = 0, 1
 CODE_UNAVAILABLE = 0xFF
-F_PROFILE, F_STRICT_IDENTITY = 1, 2
+F_PROFILE, F_STRICT_IDENTITY, F_RLC_DISTINCT = 1, 2, 4   # include/cess_bls.h CESS_BLS_F_*
 MODE_PER_SIG, MODE_RLC = 0, 1
 
 
@@ -211,12 +211,14 @@ class Context:
     """One GPU: device buffers, stream and the -G2 prepared table."""
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 20, profile: bool = False,
-                 strict_identity: bool = False, mode: int = MODE_PER_SIG, devices: Optional[Sequence[int]] = None):
+                 strict_identity: bool = False, mode: int = MODE_PER_SIG, devices: Optional[Sequence[int]] = None,
+                 rlc_distinct: bool = False):
         """devices: a list of >1 ordinals makes one context over several GPUs of
         this process (host-buffer batches sharded by index across them)."""
         lib = load_library()
         self._lib = lib
-        flags = (F_PROFILE if profile else 0) | (F_STRICT_IDENTITY if strict_identity else 0)
+        flags = (F_PROFILE if profile else 0) | (F_STRICT_IDENTITY if strict_identity else 0) | \
+            (F_RLC_DISTINCT if rlc_distinct else 0)
         ndev = len(devices) if devices is not None and len(devices) > 1 else 0
         self._devs = (ctypes.c_int * max(ndev, 1))(*(devices if ndev else [0]))
         cfg = _Config(device, max_batch, flags, mode, ndev, self._devs if ndev else None)

@@ -43,6 +43,12 @@ __global__ void k_g1_sum_segs(uint32_t, const uint64_t*, const uint64_t*, const 
 __global__ void k_rlc_pairs_list(uint32_t, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint8_t*, uint8_t*,
                                  uint8_t*, uint32_t*, uint32_t*, const uint32_t*);
 __global__ void k_fp12_prod_segs(uint32_t, const uint32_t*, const uint4*, uint64_t, uint4*, uint4*);
+__global__ void k_rlcd_records(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, uint64_t, uint32_t*, uint8_t*,
+                               uint64_t);
+__global__ void k_rlcd_s_records(uint32_t, const uint32_t*, uint8_t*, uint8_t*, uint32_t*);
+__global__ void k_fp12_prod_chunks(uint32_t, const uint64_t*, const uint64_t*, const uint8_t*, const uint4*, uint64_t,
+                                   uint4*);
+__global__ void k_fp12_mul_each(uint32_t, uint4*, const uint4*);
 __global__ void k_msm_count(uint64_t, const uint8_t*, const uint8_t*, MsmSegs, const uint32_t*, uint64_t, uint32_t*);
 __global__ void k_msm_scatter(uint64_t, const uint8_t*, const uint8_t*, MsmSegs, const uint32_t*, uint64_t, uint32_t*,
                               uint32_t*);
@@ -106,6 +112,10 @@ struct RlcState {
   DevBuf P, Q, d_perm, d_seed, part, S, Qs, pk_in, pk_code, pk_inf, pk_aff, pk_coeffs, pk_usable;
   DevBuf rec_code, rec_inf, rec_sig, rec_h, rec_f, rec_f2, acc, slots, fin_code, fin_bm, gt, gts, tmp;
   DevBuf seg, part2, rec_coeffs, lists, d_gt_all;
+  // distinct-key RLC (CESS_BLS_F_RLC_DISTINCT): every record's Miller value
+  // f_i (stride n), the chunk-product ping-pong arrays and chunk bounds
+  bool distinct = false;
+  DevBuf d_rec_f, pr_a, pr_b, pr_lo, pr_hi;
   // bucket sums of the first check (k_msm_*): records' affine points and codes
   // for the whole batch (SoA stride n), group ids, bucket tables
   bool pts = false;                 // the batch's points are kept on the device (bucket sums possible)

@@ -338,6 +338,191 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
   return CESS_BLS_OK;
 }
 
+// ---- distinct-key RLC (CESS_BLS_F_RLC_DISTINCT) -------------------------------
+// Ranges are record-index ranges [a, b) (R.perm is the identity).  A range's
+// check: S_r = sum of P_i = r_i sig_i (k_rlc_scale; identity for records with a
+// code), Miller(S_r, -G2), times the product of the range's stored f_i =
+// Miller(r_i H_i, pk_i) over its code-0 records, then one final
+// exponentiation.  The products run in chunk passes (kRlcdChunk values per
+// lane) until every range has at most 256 partials, then k_fp12_prod_segs.
+constexpr uint64_t kRlcdChunk = 32;
+static int rlcd_check(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
+                      std::vector<uint8_t>& ok, uint8_t* gt_out) {
+  hipStream_t s = c->stream;
+  const uint64_t NR = rg.size(), n = R.n;
+  R.checks += NR;
+  ok.assign(NR, 1);
+  if (NR == 0) return CESS_BLS_OK;
+  if (NR >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
+  std::vector<uint64_t> so(NR), sc(NR);
+  for (uint64_t q = 0; q < NR; q++) so[q] = rg[q].first, sc[q] = rg[q].second - rg[q].first;
+  int r = R.S.ensure(NR * 36 * 4) | R.rec_code.ensure(NR) | R.rec_inf.ensure(NR) | R.rec_sig.ensure(NR * CESS_W_G1 * 4);
+  r |= R.rec_f2.ensure(NR * CESS_W_FP12 * 4) | R.acc.ensure(NR * CESS_W_FP12 * 4);
+  r |= R.slots.ensure(NR * CESS_W_FP12 * 4 * CESS_FE_SLOTS) | R.part2.ensure(NR * kProdLanes * CESS_W_FP12 * 4);
+  r |= R.fin_code.ensure(NR) | R.fin_bm.ensure(((NR + 63) / 64) * 8) | R.gt.ensure(NR * 576);
+  if (r) return CESS_BLS_E_OOM;
+  // 1. S_r and Miller(S_r, -G2)
+  r = rlc_sums(R, s, so, sc, R.P.as<uint32_t>(), n, R.S.as<uint32_t>(), NR);
+  if (r) return r;
+  hipLaunchKernelGGL(k_rlcd_s_records, dim3((unsigned)((NR + 63) / 64)), dim3(64), 0, s, (uint32_t)NR,
+                     (const uint32_t*)R.S.as<uint32_t>(), R.rec_code.as<uint8_t>(), R.rec_inf.as<uint8_t>(),
+                     R.rec_sig.as<uint32_t>());
+  hipLaunchKernelGGL(k_miller, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, (const uint8_t*)R.rec_code.as<uint8_t>(),
+                     (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)R.rec_sig.as<uint32_t>(),
+                     (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
+                     (const uint4*)nullptr, R.rec_f2.as<uint4>(), R.slots.as<uint4>(), NR, (const uint32_t*)nullptr,
+                     NR, (const uint8_t*)nullptr);
+  HIPCHK(hipGetLastError());
+  // 2. per-range products of the stored f_i, in chunk passes
+  std::vector<uint64_t> cnt(sc), base(so);   // values per range in the current input, their first index
+  const uint4* in = R.d_rec_f.as<uint4>();
+  uint64_t in_stride = n;
+  const uint8_t* in_code = R.d_code.as<uint8_t>();
+  bool flip = false;
+  for (;;) {
+    uint64_t mx = 0;
+    for (uint64_t v : cnt) mx = std::max(mx, v);
+    if (mx <= 4 * kProdLanes && in != R.d_rec_f.as<uint4>()) break;
+    std::vector<uint64_t> lo, hi, nb(NR);
+    for (uint64_t q = 0; q < NR; q++) {
+      nb[q] = lo.size();
+      for (uint64_t a = 0; a < cnt[q]; a += kRlcdChunk) {
+        lo.push_back(base[q] + a);
+        hi.push_back(base[q] + std::min(cnt[q], a + kRlcdChunk));
+      }
+      if (cnt[q] == 0) {   // an empty range still needs its (one) partial
+        lo.push_back(base[q]);
+        hi.push_back(base[q]);
+      }
+    }
+    const uint64_t nch = lo.size();
+    if (nch >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
+    DevBuf& out = flip ? R.pr_b : R.pr_a;
+    if (out.ensure(nch * CESS_W_FP12 * 4) | R.pr_lo.ensure(nch * 8) | R.pr_hi.ensure(nch * 8)) return CESS_BLS_E_OOM;
+    HIPCHK(hipMemcpyAsync(R.pr_lo.p, lo.data(), nch * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(R.pr_hi.p, hi.data(), nch * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_fp12_prod_chunks, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, (uint32_t)nch,
+                       (const uint64_t*)R.pr_lo.as<uint64_t>(), (const uint64_t*)R.pr_hi.as<uint64_t>(), in_code, in,
+                       in_stride, out.as<uint4>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // lo / hi are host vectors
+    for (uint64_t q = 0; q < NR; q++) {
+      base[q] = nb[q];
+      cnt[q] = (q + 1 < NR ? nb[q + 1] : nch) - nb[q];
+    }
+    in = out.as<uint4>();
+    in_stride = nch;
+    in_code = nullptr;
+    flip = !flip;
+  }
+  std::vector<uint32_t> tb(NR + 1);
+  for (uint64_t q = 0; q < NR; q++) tb[q] = (uint32_t)base[q];
+  tb[NR] = (uint32_t)(base[NR - 1] + cnt[NR - 1]);
+  if (R.lists.ensure((NR + 1) * 4)) return CESS_BLS_E_OOM;
+  HIPCHK(hipMemcpyAsync(R.lists.p, tb.data(), (NR + 1) * 4, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_fp12_prod_segs, dim3((unsigned)NR), dim3((unsigned)kProdLanes), 0, s, (uint32_t)NR,
+                     (const uint32_t*)R.lists.as<uint32_t>(), in, in_stride, R.part2.as<uint4>(), R.acc.as<uint4>());
+  hipLaunchKernelGGL(k_fp12_mul_each, dim3((unsigned)((NR + 63) / 64)), dim3(64), 0, s, (uint32_t)NR,
+                     R.acc.as<uint4>(), (const uint4*)R.rec_f2.as<uint4>());
+  // 3. one final exponentiation per range
+  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
+  hipLaunchKernelGGL(k_final, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
+                     R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(), gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
+  HIPCHK(hipGetLastError());
+  std::vector<uint8_t> codes(NR);
+  HIPCHK(hipMemcpyAsync(codes.data(), R.fin_code.p, NR, hipMemcpyDeviceToHost, s));
+  if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));   // tb is a host vector
+  for (uint64_t q = 0; q < NR; q++) ok[q] = codes[q] == CODE_OK;
+  return CESS_BLS_OK;
+}
+
+// The batch's records through the per-signature light kernels in chunks of
+// qcap, then P_i, Q_i (k_rlc_scale) and f_i = Miller(Q_i, pk_i) kept for the
+// whole batch; then the batch check.
+static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint64_t index_hi, uint8_t* gt_out) {
+  hipStream_t s = c->stream;
+  const uint64_t n = R.n, q = c->qcap;
+  R.distinct = true;
+  R.K = 0;
+  R.perm.resize(n);
+  for (uint64_t i = 0; i < n; i++) R.perm[i] = (uint32_t)i;
+  int r = R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4) | R.d_code.ensure(n) | R.d_perm.ensure(n * 4);
+  r |= R.d_rec_f.ensure(n * CESS_W_FP12 * 4) | R.d_seed.ensure(32) | R.rec_h.ensure(q * CESS_W_G1 * 4);
+  r |= R.rec_inf.ensure(q);
+  StageSlot& S = c->slot[0];
+  r |= S.inf.ensure(q) | S.sig_aff.ensure(q * CESS_W_G1 * 4) | S.h_aff.ensure(q * CESS_W_G1 * 4) |
+       S.pk_aff.ensure(q * CESS_W_G2 * 4) | S.coeffs.ensure(q * (uint64_t)CESS_W_COEFFS * 4);
+  if (r) return CESS_BLS_E_OOM;
+  {
+    uint32_t sw[8];
+    for (int w = 0; w < 8; w++)
+      sw[w] = ((uint32_t)seed32[4 * w] << 24) | ((uint32_t)seed32[4 * w + 1] << 16) | ((uint32_t)seed32[4 * w + 2] << 8) |
+              seed32[4 * w + 3];
+    HIPCHK(hipMemcpyAsync(R.d_seed.p, sw, 32, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(R.d_perm.p, R.perm.data(), n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));   // sw is a stack buffer
+  }
+  const uint32_t strict = (c->flags & CESS_BLS_F_STRICT_IDENTITY) ? 1u : 0u;
+  std::vector<uint64_t> rebased;
+  for (uint64_t off = 0; off < n; off += q) {
+    const uint64_t m = std::min<uint64_t>(q, n - off);
+    const uint64_t mb0 = R.offs[off], mb1 = R.offs[off + m];
+    if (mb1 < mb0) return CESS_BLS_E_INVALID_ARG;
+    rebased.resize(m + 1);
+    for (uint64_t j = 0; j <= m; j++) {
+      if (j && R.offs[off + j] < R.offs[off + j - 1]) return CESS_BLS_E_INVALID_ARG;
+      rebased[j] = R.offs[off + j] - mb0;
+    }
+    r = c->in_sigs.ensure(m * 48) | c->in_pks.ensure(m * 96) | c->in_msgs.ensure(std::max<uint64_t>(mb1 - mb0, 1)) |
+        c->in_offs.ensure((m + 1) * 8);
+    if (r) return CESS_BLS_E_OOM;
+    HIPCHK(hipMemcpyAsync(c->in_sigs.p, R.sigs + 48 * off, m * 48, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_pks.p, R.pks + 96 * off, m * 96, hipMemcpyHostToDevice, s));
+    if (mb1 > mb0) HIPCHK(hipMemcpyAsync(c->in_msgs.p, R.msgs + mb0, mb1 - mb0, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->in_offs.p, rebased.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+    uint8_t* code = R.d_code.as<uint8_t>() + off;
+    uint8_t* inf = S.inf.as<uint8_t>();
+    HIPCHK(hipMemsetAsync(code, 0, m, s));
+    HIPCHK(hipMemsetAsync(inf, 0, m, s));
+    const unsigned g = grid_for(m);
+    // the per-signature decode / hash / prepare (run_chunk's light kernels;
+    // codes in the reference's precedence)
+    hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
+                       code, inf, S.sig_aff.as<uint32_t>(), q);
+    hipLaunchKernelGGL(k_decode_pk, dim3(g), dim3(kBlock), 0, s, m, c->in_pks.as<uint8_t>(), (const uint8_t*)nullptr,
+                       code, inf, S.pk_aff.as<uint32_t>(), q, strict);
+    hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
+                       (const uint8_t*)code, S.h_aff.as<uint32_t>(), q);
+    hipLaunchKernelGGL(k_prepare, dim3(g), dim3(kBlock), 0, s, m, (const uint32_t*)S.pk_aff.as<uint32_t>(),
+                       S.coeffs.as<uint4>(), q, code, (const uint8_t*)inf);
+    // P_i = r_i sig_i, Q_i = r_i H_i (stride n), then f_i = Miller(Q_i, pk_i)
+    hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
+                       (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
+                       (const uint32_t*)R.d_seed.as<uint32_t>(), index_hi + off, R.P.as<uint32_t>() + off,
+                       R.Q.as<uint32_t>() + off, q, n);
+    hipLaunchKernelGGL(k_rlcd_records, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
+                       (const uint32_t*)(R.Q.as<uint32_t>() + off), n, R.rec_h.as<uint32_t>(), R.rec_inf.as<uint8_t>(),
+                       q);
+    hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code,
+                       (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
+                       (const uint32_t*)R.rec_h.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
+                       (const uint4*)S.coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q,
+                       (const uint32_t*)nullptr, q, (const uint8_t*)nullptr);
+    HIPCHK(hipGetLastError());
+    // f_i rows (36 uint4 rows of stride q) into the batch-wide array (stride n)
+    HIPCHK(hipMemcpy2DAsync(R.d_rec_f.as<uint4>() + off, n * 16, c->fval.p, q * 16, m * 16, 36,
+                            hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(&R.codes[off], code, m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));   // rebased is reused by the next chunk
+  }
+  std::vector<uint8_t> ok;
+  r = rlcd_check(c, R, {{0, n}}, ok, gt_out);
+  if (r) return r;
+  R.local_ok = ok[0] != 0;
+  return CESS_BLS_OK;
+}
+
 // rlc_begin with an index base for the scalars (ranks pass rank << 40, so no
 // r_i is shared across shards under one seed)
 int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
@@ -359,6 +544,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   R.per_sig = false;
   R.K = 0;
   R.pts = R.pq = R.aos = R.have_pos = false;
+  R.distinct = false;
   R.index_hi = index_hi;
   auto gt_one = [&]() {
     if (gt_out) {   // the empty product: Gt one
@@ -374,6 +560,14 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
   hipStream_t s = c->stream;
   int r = order_begin(c, s);
   if (r) return r;
+  if (c->flags & CESS_BLS_F_RLC_DISTINCT) {
+    r = rlcd_begin(c, R, seed32, index_hi, gt_out);
+    if (r) return r;
+    r = order_end(c, s);
+    if (r) return r;
+    R.valid = true;
+    return CESS_BLS_OK;
+  }
   // 1. key groups (dedup of the 96-byte encodings; open addressing on a
   //    64-bit hash, full compare) and a counting sort by group.  Slices of the
   //    batch are deduplicated on host threads, then their distinct keys are
@@ -574,7 +768,7 @@ int cess_host::rlc_finish(cess_bls_ctx* c, uint8_t* codes_out, uint64_t* bitmap_
       }
       level.clear();
       if (!parts.empty()) {
-        int r = rlc_check_multi(c, R, parts, ok, nullptr);
+        int r = R.distinct ? rlcd_check(c, R, parts, ok, nullptr) : rlc_check_multi(c, R, parts, ok, nullptr);
         if (r) return r;
         for (size_t q = 0; q < parts.size(); q++)
           if (!ok[q]) level.push_back(parts[q]);

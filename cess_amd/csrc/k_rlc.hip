@@ -434,3 +434,69 @@ __global__ void k_gt_prod(uint32_t m, const uint8_t* __restrict__ gts, uint4* __
   }
   code[0] = is_one12(a) ? CODE_OK : CODE_PAIRING;
 }
+
+// ---- distinct-key RLC (host_rlc.cpp rlcd_*) ---------------------------------
+// Every record keeps its own Miller value f_i = Miller(Q_i, pk_i) (one pair per
+// record); a range's check multiplies its records' f_i with Miller(S_r, -G2),
+// S_r = sum r_i sig_i over the range.
+
+// k_miller input for the records of one chunk: h = affine(Q_i) (stride n, from
+// k_rlc_scale), pair 0 off (INF_SIG), pair 1 off when Q_i or the key is the
+// identity.  Records with a decode code are skipped by k_miller.
+__global__ CESS_LB void k_rlcd_records(uint64_t m, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf_in,
+                                       const uint32_t* __restrict__ Q, uint64_t qstride, uint32_t* __restrict__ h_aff,
+                                       uint8_t* __restrict__ inf_out, uint64_t stride) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  uint8_t f = INF_SIG;
+  g1a h = {fp_zero(), fp_one(), true};
+  if (code[i] == 0) {
+    h = proj_to_affine(ld_g1p(Q, qstride, i));
+    if (h.inf || (inf_in[i] & INF_PK)) f |= INF_PK;
+  } else {
+    f |= INF_PK;
+  }
+  st_fp(h_aff, stride, i, h.x);
+  st_fp(h_aff + 12 * stride, stride, i, h.y);
+  inf_out[i] = f;
+}
+
+// k_miller input for the ranges' S terms: sig = affine(S_r), pair 1 off
+__global__ void k_rlcd_s_records(uint32_t NR, const uint32_t* __restrict__ S, uint8_t* __restrict__ code,
+                                 uint8_t* __restrict__ inf, uint32_t* __restrict__ sig_aff) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= NR) return;
+  const g1a s = proj_to_affine(ld_g1p(S, NR, r));
+  st_fp(sig_aff, NR, r, s.x);
+  st_fp(sig_aff + 12 * NR, NR, r, s.y);
+  inf[r] = INF_PK | (s.inf ? INF_SIG : 0);
+  code[r] = 0;
+}
+
+// out[j] (stride nch) = product of fin[i] (stride fs) over i in [lo[j], hi[j])
+// with code[i] == 0 (code == nullptr: every i); an empty product is one
+__global__ __launch_bounds__(256) void k_fp12_prod_chunks(uint32_t nch, const uint64_t* __restrict__ lo,
+                                                          const uint64_t* __restrict__ hi,
+                                                          const uint8_t* __restrict__ code, const uint4* __restrict__ fin,
+                                                          uint64_t fs, uint4* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nch) return;
+  GlobF12 mine{out, nch, j};
+  bool first = true;
+#pragma unroll 1
+  for (uint64_t i = lo[j]; i < hi[j]; i++) {
+    if (code && code[i] != 0) continue;
+    const GlobF12 src{const_cast<uint4*>(fin), fs, (uint32_t)i};
+    if (first) copy12(mine, src);
+    else mul12(mine, src);
+    first = false;
+  }
+  if (first) set_one12(mine);
+}
+
+// a[r] <- a[r] * b[r]  (both stride NR)
+__global__ void k_fp12_mul_each(uint32_t NR, uint4* __restrict__ a, const uint4* __restrict__ b) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= NR) return;
+  mul12(GlobF12{a, NR, r}, GlobF12{const_cast<uint4*>(b), NR, r});
+}

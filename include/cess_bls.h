@@ -87,6 +87,14 @@ typedef struct cess_bls_config {
  * (PublicKey::deserialize, src/lib.rs:68-82, has no identity check), so the
  * (sig = O, pk = O) pair verifies for every message. */
 #define CESS_BLS_F_STRICT_IDENTITY 2u
+/* RLC mode for batches of (mostly) distinct keys: no key grouping; every record
+ * keeps its own Miller value Miller(r_i H(m_i), pk_i) -- one pairing per record
+ * instead of two -- the check multiplies them with Miller(sum r_i sig_i, -G2)
+ * under ONE final exponentiation, and bisection reuses the stored values (a
+ * level costs one S sum, one Miller loop and one final exponentiation per
+ * range).  Codes are those of cess_bls_verify_batch (leaves of 2,048 records
+ * are verified per signature). */
+#define CESS_BLS_F_RLC_DISTINCT 4u
 
 #define CESS_BLS_MODE_PER_SIG 0u  /* two-pairing check per signature (default; src/lib.rs:85-100)      */
 /* random linear combination with bisection (cess_bls_verify_batch_rlc semantics):

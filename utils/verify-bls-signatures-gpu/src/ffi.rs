@@ -31,6 +31,7 @@ pub const CESS_BLS_COMM_NAME_BYTES: usize = 64;
 
 pub const CESS_BLS_F_PROFILE: u32 = 1;
 pub const CESS_BLS_F_STRICT_IDENTITY: u32 = 2;
+pub const CESS_BLS_F_RLC_DISTINCT: u32 = 4;
 pub const CESS_BLS_MODE_PER_SIG: u32 = 0;
 pub const CESS_BLS_MODE_RLC: u32 = 1;
 pub const CESS_BLS_COMM_ID_BYTES: usize = 128;

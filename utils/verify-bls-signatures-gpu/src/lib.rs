@@ -112,13 +112,17 @@ pub struct Config {
     pub strict_identity: bool,
     /// what `verify_batch` runs: per-signature (default) or RLC with bisection
     pub rlc: bool,
+    /// RLC for batches of distinct keys: one pairing per record, the Miller
+    /// values kept for bisection (CESS_BLS_F_RLC_DISTINCT)
+    pub rlc_distinct: bool,
     /// several GPUs of this process (host batches sharded across them)
     pub devices: Vec<i32>,
 }
 
 impl Default for Config {
     fn default() -> Self {
-        Config { device: 0, max_batch: 1 << 20, profile: false, strict_identity: false, rlc: false, devices: vec![] }
+        Config { device: 0, max_batch: 1 << 20, profile: false, strict_identity: false, rlc: false, rlc_distinct: false,
+                 devices: vec![] }
     }
 }
 
@@ -150,7 +154,8 @@ impl Verifier {
             device: cfg.device as c_int,
             max_batch: cfg.max_batch,
             flags: (if cfg.profile { ffi::CESS_BLS_F_PROFILE } else { 0 })
-                | (if cfg.strict_identity { ffi::CESS_BLS_F_STRICT_IDENTITY } else { 0 }),
+                | (if cfg.strict_identity { ffi::CESS_BLS_F_STRICT_IDENTITY } else { 0 })
+                | (if cfg.rlc_distinct { ffi::CESS_BLS_F_RLC_DISTINCT } else { 0 }),
             mode: if cfg.rlc { ffi::CESS_BLS_MODE_RLC } else { ffi::CESS_BLS_MODE_PER_SIG },
             n_devices: if devices.len() > 1 { devices.len() as c_int } else { 0 },
             devices: if devices.len() > 1 { devices.as_ptr() } else { core::ptr::null() },

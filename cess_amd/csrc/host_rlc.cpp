@@ -14,6 +14,10 @@ using namespace cess_host;
 namespace {
 constexpr uint64_t kRlcLeaf = 2048;   // records verified per signature
 constexpr uint64_t kRlcFan = 16;      // bisection fan-out per level
+// distinct-key mode: a level re-multiplies stored Miller values and costs one
+// single-wave Miller loop and final exponentiation of latency whatever its
+// range count, so fewer, wider levels
+constexpr uint64_t kRlcdFan = 64;
 constexpr uint64_t kProdLanes = 64;   // lanes per range in the Fp12 segment product
 
 // one (range, key group) term of a batched check: perm positions [lo, hi)
@@ -345,36 +349,47 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 // Miller(r_i H_i, pk_i) over its code-0 records, then one final
 // exponentiation.  The products run in chunk passes (kRlcdChunk values per
 // lane) until every range has at most 256 partials, then k_fp12_prod_segs.
-constexpr uint64_t kRlcdChunk = 32;
-static int rlcd_check(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
-                      std::vector<uint8_t>& ok, uint8_t* gt_out) {
-  hipStream_t s = c->stream;
+constexpr uint64_t kRlcdChunk = 8;
+// Part 1 of a check, on stream t: S_r = sum of the range's P_i and
+// Miller(S_r, -G2) into R.rec_f2 (the batch's first check runs it on stream2,
+// beside the last chunk's Miller loops: the single-wave S loop is latency).
+static int rlcd_s_part(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
+                       hipStream_t t) {
   const uint64_t NR = rg.size(), n = R.n;
-  R.checks += NR;
-  ok.assign(NR, 1);
-  if (NR == 0) return CESS_BLS_OK;
-  if (NR >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
   std::vector<uint64_t> so(NR), sc(NR);
   for (uint64_t q = 0; q < NR; q++) so[q] = rg[q].first, sc[q] = rg[q].second - rg[q].first;
-  int r = R.S.ensure(NR * 36 * 4) | R.rec_code.ensure(NR) | R.rec_inf.ensure(NR) | R.rec_sig.ensure(NR * CESS_W_G1 * 4);
-  r |= R.rec_f2.ensure(NR * CESS_W_FP12 * 4) | R.acc.ensure(NR * CESS_W_FP12 * 4);
-  r |= R.slots.ensure(NR * CESS_W_FP12 * 4 * CESS_FE_SLOTS) | R.part2.ensure(NR * kProdLanes * CESS_W_FP12 * 4);
-  r |= R.fin_code.ensure(NR) | R.fin_bm.ensure(((NR + 63) / 64) * 8) | R.gt.ensure(NR * 576);
+  int r = R.S.ensure(NR * 36 * 4) | R.rec_code.ensure(NR) | R.rec_sig.ensure(NR * CESS_W_G1 * 4);
+  r |= R.rec_f2.ensure(NR * CESS_W_FP12 * 4) | R.slots.ensure(NR * CESS_W_FP12 * 4 * CESS_FE_SLOTS);
+  r |= R.fin_bm.ensure(NR);   // the S records' inf flags (k_rlcd_s_records)
   if (r) return CESS_BLS_E_OOM;
-  // 1. S_r and Miller(S_r, -G2)
-  r = rlc_sums(R, s, so, sc, R.P.as<uint32_t>(), n, R.S.as<uint32_t>(), NR);
+  r = rlc_sums(R, t, so, sc, R.P.as<uint32_t>(), n, R.S.as<uint32_t>(), NR);
   if (r) return r;
-  hipLaunchKernelGGL(k_rlcd_s_records, dim3((unsigned)((NR + 63) / 64)), dim3(64), 0, s, (uint32_t)NR,
-                     (const uint32_t*)R.S.as<uint32_t>(), R.rec_code.as<uint8_t>(), R.rec_inf.as<uint8_t>(),
+  hipLaunchKernelGGL(k_rlcd_s_records, dim3((unsigned)((NR + 63) / 64)), dim3(64), 0, t, (uint32_t)NR,
+                     (const uint32_t*)R.S.as<uint32_t>(), R.rec_code.as<uint8_t>(), R.fin_bm.as<uint8_t>(),
                      R.rec_sig.as<uint32_t>());
-  hipLaunchKernelGGL(k_miller, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, (const uint8_t*)R.rec_code.as<uint8_t>(),
-                     (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)R.rec_sig.as<uint32_t>(),
+  hipLaunchKernelGGL(k_miller, dim3(grid_for(NR)), dim3(kBlock), 0, t, NR, (const uint8_t*)R.rec_code.as<uint8_t>(),
+                     (const uint8_t*)R.fin_bm.as<uint8_t>(), (const uint32_t*)R.rec_sig.as<uint32_t>(),
                      (const uint32_t*)R.rec_sig.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
                      (const uint4*)nullptr, R.rec_f2.as<uint4>(), R.slots.as<uint4>(), NR, (const uint32_t*)nullptr,
                      NR, (const uint8_t*)nullptr);
   HIPCHK(hipGetLastError());
-  // 2. per-range products of the stored f_i, in chunk passes
-  std::vector<uint64_t> cnt(sc), base(so);   // values per range in the current input, their first index
+  return CESS_BLS_OK;
+}
+
+// Part 2, on the context stream (after part 1: `wait`, an event of part 1's
+// stream, or nullptr when part 1 ran on this stream): per-range products of
+// the stored f_i in chunk passes (kRlcdChunk values per lane) until every
+// range has at most 256 partials, then k_fp12_prod_segs, times Miller(S_r),
+// and one final exponentiation per range: ok[r] = range r passes.
+static int rlcd_final_part(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
+                           hipEvent_t wait, std::vector<uint8_t>& ok, uint8_t* gt_out) {
+  hipStream_t s = c->stream;
+  const uint64_t NR = rg.size(), n = R.n;
+  int r = R.acc.ensure(NR * CESS_W_FP12 * 4) | R.part2.ensure(NR * kProdLanes * CESS_W_FP12 * 4);
+  r |= R.fin_code.ensure(NR) | R.gt.ensure(NR * 576) | R.tmp.ensure(((NR + 63) / 64) * 8);
+  if (r) return CESS_BLS_E_OOM;
+  std::vector<uint64_t> cnt(NR), base(NR);   // values per range in the current input, their first index
+  for (uint64_t q = 0; q < NR; q++) base[q] = rg[q].first, cnt[q] = rg[q].second - rg[q].first;
   const uint4* in = R.d_rec_f.as<uint4>();
   uint64_t in_stride = n;
   const uint8_t* in_code = R.d_code.as<uint8_t>();
@@ -422,19 +437,33 @@ static int rlcd_check(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<
   HIPCHK(hipMemcpyAsync(R.lists.p, tb.data(), (NR + 1) * 4, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_fp12_prod_segs, dim3((unsigned)NR), dim3((unsigned)kProdLanes), 0, s, (uint32_t)NR,
                      (const uint32_t*)R.lists.as<uint32_t>(), in, in_stride, R.part2.as<uint4>(), R.acc.as<uint4>());
+  if (wait) HIPCHK(hipStreamWaitEvent(s, wait, 0));
   hipLaunchKernelGGL(k_fp12_mul_each, dim3((unsigned)((NR + 63) / 64)), dim3(64), 0, s, (uint32_t)NR,
                      R.acc.as<uint4>(), (const uint4*)R.rec_f2.as<uint4>());
-  // 3. one final exponentiation per range
   HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
   hipLaunchKernelGGL(k_final, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
-                     R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(), gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
+                     R.slots.as<uint4>(), R.tmp.as<uint64_t>(), gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
   HIPCHK(hipGetLastError());
   std::vector<uint8_t> codes(NR);
   HIPCHK(hipMemcpyAsync(codes.data(), R.fin_code.p, NR, hipMemcpyDeviceToHost, s));
   if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));   // tb is a host vector
+  ok.assign(NR, 1);
   for (uint64_t q = 0; q < NR; q++) ok[q] = codes[q] == CODE_OK;
   return CESS_BLS_OK;
+}
+
+// A check of the record ranges rg (both parts on the context stream).
+static int rlcd_check(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<uint64_t, uint64_t>>& rg,
+                      std::vector<uint8_t>& ok, uint8_t* gt_out) {
+  const uint64_t NR = rg.size();
+  R.checks += NR;
+  ok.assign(NR, 1);
+  if (NR == 0) return CESS_BLS_OK;
+  if (NR >= (1ull << 31)) return CESS_BLS_E_INVALID_ARG;
+  int r = rlcd_s_part(c, R, rg, c->stream);
+  if (r) return r;
+  return rlcd_final_part(c, R, rg, nullptr, ok, gt_out);
 }
 
 // The batch's records through the per-signature light kernels in chunks of
@@ -501,6 +530,16 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
                        (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
                        (const uint32_t*)R.d_seed.as<uint32_t>(), index_hi + off, R.P.as<uint32_t>() + off,
                        R.Q.as<uint32_t>() + off, q, n);
+    if (off + m == n) {
+      // the last chunk: every P_i exists now, so the batch's S sum and its
+      // single-wave Miller loop run on stream2 beside this chunk's Miller loops
+      HIPCHK(hipEventRecord(c->ev_start, s));
+      HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+      R.checks += 1;
+      r = rlcd_s_part(c, R, {{0, n}}, c->stream2);
+      if (r) return r;
+      HIPCHK(hipEventRecord(c->ev_light[0], c->stream2));
+    }
     hipLaunchKernelGGL(k_rlcd_records, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
                        (const uint32_t*)(R.Q.as<uint32_t>() + off), n, R.rec_h.as<uint32_t>(), R.rec_inf.as<uint8_t>(),
                        q);
@@ -517,7 +556,7 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
     HIPCHK(hipStreamSynchronize(s));   // rebased is reused by the next chunk
   }
   std::vector<uint8_t> ok;
-  r = rlcd_check(c, R, {{0, n}}, ok, gt_out);
+  r = rlcd_final_part(c, R, {{0, n}}, c->ev_light[0], ok, gt_out);
   if (r) return r;
   R.local_ok = ok[0] != 0;
   return CESS_BLS_OK;
@@ -763,7 +802,7 @@ int cess_host::rlc_finish(cess_bls_ctx* c, uint8_t* codes_out, uint64_t* bitmap_
           leaves.push_back(w);
           continue;
         }
-        const uint64_t fan = std::min<uint64_t>(kRlcFan, (len + kRlcLeaf - 1) / kRlcLeaf);
+        const uint64_t fan = std::min<uint64_t>(R.distinct ? kRlcdFan : kRlcFan, (len + kRlcLeaf - 1) / kRlcLeaf);
         for (uint64_t q = 0; q < fan; q++) parts.push_back({w.first + len * q / fan, w.first + len * (q + 1) / fan});
       }
       level.clear();

@@ -238,7 +238,7 @@ static int rlc_scale_all(cess_bls_ctx* c, RlcState& R) {
   hipLaunchKernelGGL(k_rlc_scale, dim3(grid_for(R.n)), dim3(kBlock), 0, s, R.n, (const uint8_t*)R.d_code.as<uint8_t>(),
                      (const uint8_t*)R.d_inf.as<uint8_t>(), (const uint32_t*)R.Xs.as<uint32_t>(),
                      (const uint32_t*)R.Xh.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(), R.index_hi,
-                     R.P.as<uint32_t>(), R.Q.as<uint32_t>(), R.n, R.n);
+                     R.P.as<uint32_t>(), R.Q.as<uint32_t>(), R.n, R.n, 4u);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   R.pq = true;
@@ -343,6 +343,10 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 }
 
 // ---- distinct-key RLC (CESS_BLS_F_RLC_DISTINCT) -------------------------------
+// Scalars: the low 64 bits of the record's rlc_scalar (k_rlc_scale kwords 2),
+// so an invalid batch passes a check with probability <= 2^-64 (the random
+// exponent size of BLS batch verification in Ethereum consensus clients);
+// half the per-record scalar multiplication of the 128-bit form.
 // Ranges are record-index ranges [a, b) (R.perm is the identity).  A range's
 // check: S_r = sum of P_i = r_i sig_i (k_rlc_scale; identity for records with a
 // code), Miller(S_r, -G2), times the product of the range's stored f_i =
@@ -529,7 +533,7 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
     hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
                        (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
                        (const uint32_t*)R.d_seed.as<uint32_t>(), index_hi + off, R.P.as<uint32_t>() + off,
-                       R.Q.as<uint32_t>() + off, q, n);
+                       R.Q.as<uint32_t>() + off, q, n, 2u);
     if (off + m == n) {
       // the last chunk: every P_i exists now, so the batch's S sum and its
       // single-wave Miller loop run on stream2 beside this chunk's Miller loops
@@ -731,7 +735,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
       hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)c->code.as<uint8_t>(),
                          (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
                          (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)R.d_seed.as<uint32_t>(),
-                         index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->qcap, (uint64_t)n);
+                         index_hi + off, R.P.as<uint32_t>() + off, R.Q.as<uint32_t>() + off, c->qcap, (uint64_t)n, 4u);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // hc/hi are reused by the next chunk

@@ -67,13 +67,15 @@ __device__ void rlc_scalar(const uint32_t* seed, uint64_t i, uint32_t (&k)[4]) {
 // (branch-relaxation scavenging) defect, not a data race: the product library
 // therefore contains no device calls at all (tests/test_isa_guard.py checks
 // the shipped code objects for s_swappc_b64).
-__device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint32_t (&k)[4]) {
+// (kwords = 4: the 128-bit scalar; 2: its low 64 bits -- the distinct-key
+// mode's scalars, 32 windows instead of 64)
+__device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint32_t (&k)[4], int kwords = 4) {
   const g1p T1 = {px, py, fp_one()};
   const g1p T2 = proj_dbl(T1);
   const g1p T3 = proj_add_mixed(T2, px, py);
   g1p acc = proj_identity<fp>();
 #pragma unroll 1
-  for (int w = 3; w >= 0; w--) {
+  for (int w = kwords - 1; w >= 0; w--) {
 #pragma unroll 1
     for (int b = 30; b >= 0; b -= 2) {
       acc = proj_dbl(proj_dbl(acc));
@@ -90,7 +92,7 @@ __device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint3
 __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
                                     const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
                                     const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
-                                    uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride) {
+                                    uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride, uint32_t kwords) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g1p p = proj_identity<fp>(), q = proj_identity<fp>();
@@ -98,8 +100,10 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   if (code[i] == 0) {
     uint32_t k[4];
     rlc_scalar(seed, index_base + i, k);
-    if ((fl & INF_SIG) == 0) p = mul128_w2(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), k);
-    if ((fl & INF_PK) == 0) q = mul128_w2(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), k);
+    const int kw = kwords == 2 ? 2 : 4;
+    if (kw == 2) k[2] = k[3] = 0;
+    if ((fl & INF_SIG) == 0) p = mul128_w2(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), k, kw);
+    if ((fl & INF_PK) == 0) q = mul128_w2(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), k, kw);
   }
   st_g1p(P, out_stride, i, p);
   st_g1p(Q, out_stride, i, q);

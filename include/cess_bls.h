@@ -93,7 +93,10 @@ typedef struct cess_bls_config {
  * under ONE final exponentiation, and bisection reuses the stored values (a
  * level costs one S sum, one Miller loop and one final exponentiation per
  * range).  Codes are those of cess_bls_verify_batch (leaves of 2,048 records
- * are verified per signature). */
+ * are verified per signature).  Its random exponents are 64-bit (a check
+ * passes an invalid batch with probability <= 2^-64, the size Ethereum
+ * consensus clients use for BLS batch verification); the key-grouped mode's
+ * are 128-bit. */
 #define CESS_BLS_F_RLC_DISTINCT 4u
 
 #define CESS_BLS_MODE_PER_SIG 0u  /* two-pairing check per signature (default; src/lib.rs:85-100)      */

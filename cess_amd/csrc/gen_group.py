@@ -114,10 +114,12 @@ class H:
 
 
 class Graph:
-    def __init__(self):
+    def __init__(self, pool=None):
         self.kind = []      # "in", "const", "mul", "sqr", "lin", "inv"
         self.args = []
-        self.consts = []    # Fp2 integer values of const nodes (pool order)
+        self.consts = list(pool) if pool else []   # Fp2 integer values of const nodes (pool order)
+        # pool: another program's constant pool, shared (its indices kept)
+        self.pool_index = {v: i for i, v in enumerate(self.consts)}
         self.const_of = {}
         self.inputs = {}    # name -> node
         self.outputs = {}   # name -> node (+ sign folded by the caller)
@@ -135,8 +137,10 @@ class Graph:
     def const(self, v):
         v = (v[0] % P, v[1] % P)
         if v not in self.const_of:
-            self.const_of[v] = self._new("const", len(self.consts))
-            self.consts.append(v)
+            if v not in self.pool_index:
+                self.pool_index[v] = len(self.consts)
+                self.consts.append(v)
+            self.const_of[v] = self._new("const", self.pool_index[v])
         return H(self.const_of[v])
 
     # operands of MUL / SQR: a handle, or a 2-term sum of handles
@@ -505,6 +509,18 @@ def build():
     return g
 
 
+def build_fe(pool):
+    """The final exponentiation alone (k_group_fe: one Miller-loop value or
+    product per wave, the RLC checks): inputs f0..f5 (w-basis), outputs
+    gt0..gt5; constants from the full program's pool (same indices)."""
+    g = Graph(pool)
+    f = [g.inp(f"f{i}") for i in range(6)]
+    gt = final_exp(g, f)
+    for i in range(6):
+        g.out(f"gt{i}", gt[i])
+    return g
+
+
 # --- scheduling --------------------------------------------------------------
 def deps(g, n):
     k, a = g.kind[n], g.args[n]
@@ -729,12 +745,48 @@ def simulate(g, rounds, slot, nslots, inputs):
     return {name: S[slot[n]] for name, n in g.outputs.items()}
 
 
-def generate():
-    g = build()
+def generate(g=None):
+    g = g or build()
     rounds, done = schedule(g)
     slot, nslots = allocate(g, rounds, done)
     heads, ents = encode(g, rounds, slot)
     return g, rounds, slot, nslots, heads, ents
+
+
+def write_fe(full):
+    """bls/group_fe_prog.hpp: the final-exponentiation program (namespace
+    grpfe; its constants are grp::kConsts)."""
+    g, rounds, slot, nslots, heads, ents = generate(build_fe(full.consts))
+    assert len(g.consts) == len(full.consts), "the FE program needs no new constants"
+    out = []
+    w = out.append
+    w("// GENERATED by cess_amd/csrc/gen_group.py -- do not edit.")
+    w("// Lane-group final exponentiation (k_group_fe, k_group.hip): the RLC checks'")
+    w(f"// one value per wave.  {len(heads)} rounds, {nslots} LDS Fp2 slots; constants: grp::kConsts.")
+    w("#pragma once")
+    w('#include "group_prog.hpp"')
+    w("namespace grpfe {")
+    w(f"constexpr int N_ROUNDS = {len(heads)};")
+    w(f"constexpr int N_SLOTS = {nslots};")
+    w(f"constexpr int N_ENTS = {len(ents)};")
+    for i in range(6):
+        w(f"constexpr int IN_F{i} = {slot[g.inputs[f'f{i}']]};")
+    for i in range(6):
+        w(f"constexpr int OUT_GT{i} = {slot[g.outputs[f'gt{i}']]};")
+    w("CESS_GRP_DATA uint32_t kRounds[N_ROUNDS] = {")
+    for i in range(0, len(heads), 8):
+        w("  " + ", ".join(f"0x{(k | (n << 8) | (off << 16)):08x}u" for k, n, off in heads[i:i + 8]) + ",")
+    w("};")
+    w("CESS_GRP_DATA uint32_t kEnts[N_ENTS][4] = {")
+    for e in ents:
+        words = [e[4 * q] | (e[4 * q + 1] << 8) | (e[4 * q + 2] << 16) | (e[4 * q + 3] << 24) for q in range(4)]
+        w("  {" + ", ".join(f"0x{x:08x}u" for x in words) + "},")
+    w("};")
+    w("}  // namespace grpfe")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bls", "group_fe_prog.hpp")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+    print("wrote", path, f"({len(heads)} rounds, {nslots} slots, {len(ents)} entries)")
 
 
 def limbs(v, n=12):
@@ -793,6 +845,7 @@ def main():
         f.write("\n".join(out) + "\n")
     print("wrote", path, f"({len(heads)} rounds, {nslots} slots, {len(ents)} entries)")
     print({OP_NAMES[k]: (cnt[k], ops[k]) for k in OP_NAMES})
+    write_fe(g)
 
 
 if __name__ == "__main__":

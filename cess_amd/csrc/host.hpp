@@ -49,6 +49,7 @@ __global__ void k_rlcd_s_records(uint32_t, const uint32_t*, uint8_t*, uint8_t*, 
 __global__ void k_fp12_prod_chunks(uint32_t, const uint64_t*, const uint64_t*, const uint8_t*, const uint4*, uint64_t,
                                    uint4*);
 __global__ void k_fp12_mul_each(uint32_t, uint4*, const uint4*);
+__global__ void k_group_fe(uint32_t, const uint4*, uint8_t*, uint8_t*);
 __global__ void k_msm_count(uint64_t, const uint8_t*, const uint8_t*, MsmSegs, const uint32_t*, uint64_t, uint32_t*);
 __global__ void k_msm_scatter(uint64_t, const uint8_t*, const uint8_t*, MsmSegs, const uint32_t*, uint64_t, uint32_t*,
                               uint32_t*);

@@ -143,6 +143,28 @@ static bool msm_ok(uint64_t covered, uint64_t segs) {
   return e == 1 || covered >= 64 * segs;
 }
 
+// Final exponentiation + identity test of a check's NR products (R.acc,
+// stride NR) into R.fin_code (and R.gt when gt): one WAVE per product
+// (k_group_fe, the lane-group program: a check's latency is one value's final
+// exponentiation, ~10 ms for one lane of k_final), or env CESS_BLS_RLC_FE=lane
+// one lane per product (k_final; tests compare the two).
+static bool rlc_fe_lane() {
+  const char* e = getenv("CESS_BLS_RLC_FE");
+  return e && strcmp(e, "lane") == 0;
+}
+static int rlc_final_exp(cess_bls_ctx* c, RlcState& R, uint64_t NR, hipStream_t s, bool gt) {
+  if (rlc_fe_lane()) {
+    HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
+    hipLaunchKernelGGL(k_final, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
+                       R.slots.as<uint4>(), R.tmp.as<uint64_t>(), gt ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
+  } else {
+    hipLaunchKernelGGL(k_group_fe, dim3((unsigned)NR), dim3(64), 0, s, (uint32_t)NR, (const uint4*)R.acc.as<uint4>(),
+                       R.fin_code.as<uint8_t>(), gt ? R.gt.as<uint8_t>() : (uint8_t*)nullptr);
+  }
+  HIPCHK(hipGetLastError());
+  return CESS_BLS_OK;
+}
+
 // Sums of one check from the batch's points: S[q] = sum_{i in part q} r_i sig_i
 // (stride NR), Qs[t] = sum_{i in term t} r_i H_i (stride M), over the records
 // with code 0 (identity terms excluded).  Count entries per bucket, lay the
@@ -330,10 +352,9 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
                      R.rec_f.as<uint4>(), R.rec_f2.as<uint4>(), M, d_group, (uint64_t)R.K, (const uint8_t*)nullptr);
   hipLaunchKernelGGL(k_fp12_prod_segs, dim3((unsigned)NR), dim3((unsigned)kProdLanes), 0, s, (uint32_t)NR, d_tbeg,
                      (const uint4*)R.rec_f.as<uint4>(), (uint64_t)M, R.part2.as<uint4>(), R.acc.as<uint4>());
-  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
-  hipLaunchKernelGGL(k_final, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
-                     R.slots.as<uint4>(), R.fin_bm.as<uint64_t>(), gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
-  HIPCHK(hipGetLastError());
+  if (R.tmp.ensure(((NR + 63) / 64) * 8)) return CESS_BLS_E_OOM;
+  r = rlc_final_exp(c, R, NR, s, gt_out != nullptr);
+  if (r) return r;
   std::vector<uint8_t> codes(NR);
   HIPCHK(hipMemcpyAsync(codes.data(), R.fin_code.p, NR, hipMemcpyDeviceToHost, s));
   if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));
@@ -444,10 +465,8 @@ static int rlcd_final_part(cess_bls_ctx* c, RlcState& R, const std::vector<std::
   if (wait) HIPCHK(hipStreamWaitEvent(s, wait, 0));
   hipLaunchKernelGGL(k_fp12_mul_each, dim3((unsigned)((NR + 63) / 64)), dim3(64), 0, s, (uint32_t)NR,
                      R.acc.as<uint4>(), (const uint4*)R.rec_f2.as<uint4>());
-  HIPCHK(hipMemsetAsync(R.fin_code.p, 0, NR, s));
-  hipLaunchKernelGGL(k_final, dim3(grid_for(NR)), dim3(kBlock), 0, s, NR, R.fin_code.as<uint8_t>(), R.acc.as<uint4>(),
-                     R.slots.as<uint4>(), R.tmp.as<uint64_t>(), gt_out ? R.gt.as<uint8_t>() : (uint8_t*)nullptr, NR);
-  HIPCHK(hipGetLastError());
+  r = rlc_final_exp(c, R, NR, s, gt_out != nullptr);
+  if (r) return r;
   std::vector<uint8_t> codes(NR);
   HIPCHK(hipMemcpyAsync(codes.data(), R.fin_code.p, NR, hipMemcpyDeviceToHost, s));
   if (gt_out) HIPCHK(hipMemcpyAsync(gt_out, R.gt.p, 576, hipMemcpyDeviceToHost, s));

@@ -116,3 +116,40 @@ def test_rlcd_empty_and_tiny(dctx, ctx):
     msgs[1] = bytes(32)
     codes, words, st = dctx.verify_rlc(*_pack(sigs, pks, msgs), seed=bytes(32))
     assert list(codes) == [0, 5, 0]
+
+
+def test_rlc_group_fe_equals_lane_fe(ctx, dctx, monkeypatch):
+    """The RLC checks' final exponentiation runs one WAVE per value (k_group_fe,
+    the lane-group program); env CESS_BLS_RLC_FE=lane selects the one-lane
+    k_final.  Both give the same Gt bytes, on the distinct-key check and on the
+    key-grouped check, for a failing and a passing batch."""
+    from cess_amd import bls
+    sigs, pks, msgs = _distinct_batch(ctx, 3000, 17)
+    good = _pack(sigs, pks, msgs)
+    msgs[123] = bytes(32)
+    bad = _pack(sigs, pks, msgs)
+    grouped = bls.Context(max_batch=1 << 12)
+    owner = [i % 4 for i in range(800)]
+    gs = [sigs[o] for o in owner]   # placeholder signatures, replaced below
+    try:
+        rng = random.Random(18)
+        sks = [rng.randrange(1, R).to_bytes(32, "big") for _ in range(4)]
+        kp = ctx.public_keys(sks)
+        gm = [rng.randbytes(32) for _ in range(800)]
+        gs = ctx.sign([sks[o] for o in owner], gm)
+        gm[5] = bytes(32)
+        gbad = _pack(gs, [kp[o] for o in owner], gm)
+        out = {}
+        for fe in ("group", "lane"):
+            if fe == "lane":
+                monkeypatch.setenv("CESS_BLS_RLC_FE", "lane")
+            res = []
+            for c, packed in ((dctx, bad), (dctx, good), (grouped, gbad)):
+                res.append(c.rlc_begin(*packed, seed=bytes([3]) * 32))
+                c.rlc_finish(False)
+            out[fe] = res
+    finally:
+        grouped.close()
+    one = bytes(47) + b"\x01" + bytes(576 - 48)
+    assert out["group"] == out["lane"]
+    assert out["group"][0] != one and out["group"][1] == one and out["group"][2] != one

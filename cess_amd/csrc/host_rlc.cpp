@@ -364,10 +364,12 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 }
 
 // ---- distinct-key RLC (CESS_BLS_F_RLC_DISTINCT) -------------------------------
-// Scalars: the low 64 bits of the record's rlc_scalar (k_rlc_scale kwords 2),
-// so an invalid batch passes a check with probability <= 2^-64 (the random
-// exponent size of BLS batch verification in Ethereum consensus clients);
-// half the per-record scalar multiplication of the 128-bit form.
+// Scalars: r_i = a + b lambda with 32-bit a (odd), b from the record's
+// rlc_scalar and lambda phi's eigenvalue on G1 (k_rlc_scale kwords 1,
+// mul_glv32): 2^63 values, so an invalid batch passes a check with
+// probability <= 2^-63 (Ethereum consensus clients batch BLS with 64-bit
+// exponents), for 32 doublings + 32 additions per point instead of the
+// 128-bit form's 128 + 64.
 // Ranges are record-index ranges [a, b) (R.perm is the identity).  A range's
 // check: S_r = sum of P_i = r_i sig_i (k_rlc_scale; identity for records with a
 // code), Miller(S_r, -G2), times the product of the range's stored f_i =
@@ -552,7 +554,7 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
     hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
                        (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
                        (const uint32_t*)R.d_seed.as<uint32_t>(), index_hi + off, R.P.as<uint32_t>() + off,
-                       R.Q.as<uint32_t>() + off, q, n, 2u);
+                       R.Q.as<uint32_t>() + off, q, n, 1u);
     if (off + m == n) {
       // the last chunk: every P_i exists now, so the batch's S sum and its
       // single-wave Miller loop run on stream2 beside this chunk's Miller loops

@@ -89,6 +89,34 @@ __device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint3
   return acc;
 }
 
+// [a + b lambda]P for 32-bit a, b, where lambda is the eigenvalue of
+// phi(x, y) = (beta x, y) on G1 (curve.hpp: phi = [-x^2]): 2-bit joint
+// windows over {P, 2P, 3P} and their phi images (beta times the x
+// coordinate of the selected entry, projective (X : Y : Z) -> (beta X : Y : Z)):
+// 32 doublings + 32 complete additions, against 64 + 32 for a 64-bit scalar.
+// The distinct-key RLC mode's scalars (2^63 values: soundness 2^-63 per check).
+__device__ __forceinline__ g1p mul_glv32(const fp& px, const fp& py, uint32_t a, uint32_t b) {
+  const g1p T1 = {px, py, fp_one()};
+  const g1p T2 = proj_dbl(T1);
+  const g1p T3 = proj_add_mixed(T2, px, py);
+  const fp beta = fp_from(c::G1_BETA);
+  g1p acc = proj_identity<fp>();
+#pragma unroll 1
+  for (int bp = 30; bp >= 0; bp -= 2) {
+    acc = proj_dbl(proj_dbl(acc));
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+      const uint32_t d = ((h ? b : a) >> bp) & 3u;
+      g1p t = {select(d == 1, T1.x, select(d == 2, T2.x, T3.x)), select(d == 1, T1.y, select(d == 2, T2.y, T3.y)),
+               select(d == 1, T1.z, select(d == 2, T2.z, T3.z))};
+      if (h) t.x = mul(t.x, beta);
+      const g1p sum = proj_add(acc, t);
+      acc = {select(d != 0, sum.x, acc.x), select(d != 0, sum.y, acc.y), select(d != 0, sum.z, acc.z)};
+    }
+  }
+  return acc;
+}
+
 __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
                                     const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
                                     const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
@@ -100,10 +128,16 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   if (code[i] == 0) {
     uint32_t k[4];
     rlc_scalar(seed, index_base + i, k);
-    const int kw = kwords == 2 ? 2 : 4;
-    if (kw == 2) k[2] = k[3] = 0;
-    if ((fl & INF_SIG) == 0) p = mul128_w2(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), k, kw);
-    if ((fl & INF_PK) == 0) q = mul128_w2(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), k, kw);
+    if (kwords == 1) {   // r_i = a + b lambda, a = k[0] | 1, b = k[1] (mul_glv32)
+      const uint32_t a = k[0] | 1u, b = k[1];
+      if ((fl & INF_SIG) == 0) p = mul_glv32(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), a, b);
+      if ((fl & INF_PK) == 0) q = mul_glv32(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), a, b);
+    } else {
+      const int kw = kwords == 2 ? 2 : 4;
+      if (kw == 2) k[2] = k[3] = 0;
+      if ((fl & INF_SIG) == 0) p = mul128_w2(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), k, kw);
+      if ((fl & INF_PK) == 0) q = mul128_w2(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), k, kw);
+    }
   }
   st_g1p(P, out_stride, i, p);
   st_g1p(Q, out_stride, i, q);

@@ -93,9 +93,10 @@ typedef struct cess_bls_config {
  * under ONE final exponentiation, and bisection reuses the stored values (a
  * level costs one S sum, one Miller loop and one final exponentiation per
  * range).  Codes are those of cess_bls_verify_batch (leaves of 2,048 records
- * are verified per signature).  Its random exponents are 64-bit (a check
- * passes an invalid batch with probability <= 2^-64, the size Ethereum
- * consensus clients use for BLS batch verification); the key-grouped mode's
+ * are verified per signature).  Its random exponents take 2^63 values
+ * (a + b lambda with 32-bit a, b and lambda the G1 endomorphism's eigenvalue:
+ * a check passes an invalid batch with probability <= 2^-63; Ethereum
+ * consensus clients batch BLS with 64-bit exponents); the key-grouped mode's
  * are 128-bit. */
 #define CESS_BLS_F_RLC_DISTINCT 4u
 

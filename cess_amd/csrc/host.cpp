@@ -97,7 +97,10 @@ static int alloc_stage(cess_bls_ctx* c) {
 // measured SLOWER on MI355X (1.970 M sigs/s unpipelined vs 1.914 / 1.873 /
 // 1.879 M at 512K / 256K / 128K parts, profiles/r02c_sweep_launch_records.txt:
 // k_miller slows from 187 to 263 ms per 1 M when co-resident waves share its
-// SIMDs), so the mechanism stays available via CESS_BLS_LAUNCH_RECORDS only.
+// SIMDs; re-measured with the round-5 kernels: 2.74 M unpipelined vs 2.65 /
+// 2.51 M at 512K / 256K parts, k_miller 149 -> 200 ms,
+// profiles/round5_al_sweep_launch_records.txt), so the mechanism stays
+// available via CESS_BLS_LAUNCH_RECORDS only.
 static uint64_t launch_records(uint64_t cap) {
   uint64_t q = cap;
   if (const char* e = getenv("CESS_BLS_LAUNCH_RECORDS")) q = strtoull(e, nullptr, 10);

@@ -867,7 +867,9 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
 // pt(pair) yields the pair's affine G1 point; src(pair, step) its coefficients.
 // norm1: pair 1's lines are normalised to c2 = 1 as well (a distinct-key table
 // after normalize_lines); otherwise they take the general sparse product.
-template <class S, class Pt, class Src, class DG = NoDiag>
+// GEN0: pair 0's lines are general too (two per-record tables: the
+// distinct-key RLC's two records per lane, k_miller_rr).
+template <bool GEN0 = false, class S, class Pt, class Src, class DG = NoDiag>
 CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1 = false,
                                  DG* dg = nullptr) {
   set_one12(f);
@@ -887,10 +889,14 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
       if (dg) {
         if (pr) dg->template mark<0>(); else dg->template mark<2>();
       }
-      if (pr && !norm1)
+      if constexpr (GEN0) {
         mul014(f, k.c2, c1, c4);
-      else
-        mul014_one(f, c1, c4);   // -G2 table (and normalised key tables): c2 = 1
+      } else {
+        if (pr && !norm1)
+          mul014(f, k.c2, c1, c4);
+        else
+          mul014_one(f, c1, c4);   // -G2 table (and normalised key tables): c2 = 1
+      }
       CESS_MEMBAR();
       if (dg) {
         if (pr) dg->template mark<1>(); else dg->template mark<3>();

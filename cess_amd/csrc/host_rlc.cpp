@@ -370,13 +370,15 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 // probability <= 2^-63 (Ethereum consensus clients batch BLS with 64-bit
 // exponents), for 32 doublings + 32 additions per point instead of the
 // 128-bit form's 128 + 64.
-// Ranges are record-index ranges [a, b) (R.perm is the identity).  A range's
-// check: S_r = sum of P_i = r_i sig_i (k_rlc_scale; identity for records with a
-// code), Miller(S_r, -G2), times the product of the range's stored f_i =
-// Miller(r_i H_i, pk_i) over its code-0 records, then one final
-// exponentiation.  The products run in chunk passes (kRlcdChunk values per
+// Ranges are record-index ranges [a, b) (R.perm is the identity) whose start
+// and end (unless n) are multiples of kRlcdPer.  A range's check: S_r = sum of
+// P_i = r_i sig_i (k_rlc_scale; identity for records with a code),
+// Miller(S_r, -G2), times the product of the range's stored lane values g_k =
+// prod f_i over i in [kRlcdPer k, kRlcdPer (k + 1)), f_i = Miller(r_i H_i, pk_i)
+// (k_miller_rr; one for records with a code), then one final exponentiation.  The products run in chunk passes (kRlcdChunk values per
 // lane) until every range has at most 256 partials, then k_fp12_prod_segs.
 constexpr uint64_t kRlcdChunk = 8;
+constexpr uint64_t kRlcdPer = CESS_RLCD_PER;
 // Part 1 of a check, on stream t: S_r = sum of the range's P_i and
 // Miller(S_r, -G2) into R.rec_f2 (the batch's first check runs it on stream2,
 // beside the last chunk's Miller loops: the single-wave S loop is latency).
@@ -416,10 +418,16 @@ static int rlcd_final_part(cess_bls_ctx* c, RlcState& R, const std::vector<std::
   r |= R.fin_code.ensure(NR) | R.gt.ensure(NR * 576) | R.tmp.ensure(((NR + 63) / 64) * 8);
   if (r) return CESS_BLS_E_OOM;
   std::vector<uint64_t> cnt(NR), base(NR);   // values per range in the current input, their first index
-  for (uint64_t q = 0; q < NR; q++) base[q] = rg[q].first, cnt[q] = rg[q].second - rg[q].first;
+  for (uint64_t q = 0; q < NR; q++) {
+    // record range [a, b) -> lane values [a / P, ceil(b / P))
+    if (rg[q].first % kRlcdPer || (rg[q].second % kRlcdPer && rg[q].second != n) || rg[q].second < rg[q].first)
+      return CESS_BLS_E_INVALID_ARG;
+    base[q] = rg[q].first / kRlcdPer;
+    cnt[q] = (rg[q].second + kRlcdPer - 1) / kRlcdPer - base[q];
+  }
   const uint4* in = R.d_rec_f.as<uint4>();
-  uint64_t in_stride = n;
-  const uint8_t* in_code = R.d_code.as<uint8_t>();
+  uint64_t in_stride = (n + kRlcdPer - 1) / kRlcdPer;
+  const uint8_t* in_code = nullptr;
   bool flip = false;
   for (;;) {
     uint64_t mx = 0;
@@ -502,7 +510,7 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
   R.perm.resize(n);
   for (uint64_t i = 0; i < n; i++) R.perm[i] = (uint32_t)i;
   int r = R.P.ensure(n * 36 * 4) | R.Q.ensure(n * 36 * 4) | R.d_code.ensure(n) | R.d_perm.ensure(n * 4);
-  r |= R.d_rec_f.ensure(n * CESS_W_FP12 * 4) | R.d_seed.ensure(32) | R.rec_h.ensure(q * CESS_W_G1 * 4);
+  r |= R.d_rec_f.ensure(((n + kRlcdPer - 1) / kRlcdPer) * CESS_W_FP12 * 4) | R.d_seed.ensure(32) | R.rec_h.ensure(q * CESS_W_G1 * 4);
   r |= R.rec_inf.ensure(q);
   StageSlot& S = c->slot[0];
   r |= S.inf.ensure(q) | S.sig_aff.ensure(q * CESS_W_G1 * 4) | S.h_aff.ensure(q * CESS_W_G1 * 4) |
@@ -519,8 +527,10 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
   }
   const uint32_t strict = (c->flags & CESS_BLS_F_STRICT_IDENTITY) ? 1u : 0u;
   std::vector<uint64_t> rebased;
-  for (uint64_t off = 0; off < n; off += q) {
-    const uint64_t m = std::min<uint64_t>(q, n - off);
+  // chunks start at multiples of kRlcdPer (k_miller_rr's lanes)
+  const uint64_t step = q >= kRlcdPer ? q - q % kRlcdPer : q;
+  for (uint64_t off = 0; off < n; off += step) {
+    const uint64_t m = std::min<uint64_t>(step, n - off);
     const uint64_t mb0 = R.offs[off], mb1 = R.offs[off + m];
     if (mb1 < mb0) return CESS_BLS_E_INVALID_ARG;
     rebased.resize(m + 1);
@@ -568,15 +578,13 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
     hipLaunchKernelGGL(k_rlcd_records, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
                        (const uint32_t*)(R.Q.as<uint32_t>() + off), n, R.rec_h.as<uint32_t>(), R.rec_inf.as<uint8_t>(),
                        q);
-    hipLaunchKernelGGL(k_miller, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code,
-                       (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
-                       (const uint32_t*)R.rec_h.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
-                       (const uint4*)S.coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q,
-                       (const uint32_t*)nullptr, q, (const uint8_t*)nullptr);
+    // g_k straight into the batch-wide lane values (stride ceil(n / P))
+    const uint64_t np = (m + kRlcdPer - 1) / kRlcdPer;
+    hipLaunchKernelGGL(k_miller_rr, dim3(grid_for(np)), dim3(kBlock), 0, s, np, m, (const uint8_t*)code,
+                       (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
+                       (const uint4*)S.coeffs.as<uint4>(), R.d_rec_f.as<uint4>() + off / kRlcdPer, q,
+                       (n + kRlcdPer - 1) / kRlcdPer);
     HIPCHK(hipGetLastError());
-    // f_i rows (36 uint4 rows of stride q) into the batch-wide array (stride n)
-    HIPCHK(hipMemcpy2DAsync(R.d_rec_f.as<uint4>() + off, n * 16, c->fval.p, q * 16, m * 16, 36,
-                            hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(&R.codes[off], code, m, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));   // rebased is reused by the next chunk
   }
@@ -828,7 +836,11 @@ int cess_host::rlc_finish(cess_bls_ctx* c, uint8_t* codes_out, uint64_t* bitmap_
           continue;
         }
         const uint64_t fan = std::min<uint64_t>(R.distinct ? kRlcdFan : kRlcFan, (len + kRlcLeaf - 1) / kRlcLeaf);
-        for (uint64_t q = 0; q < fan; q++) parts.push_back({w.first + len * q / fan, w.first + len * (q + 1) / fan});
+        // distinct-key ranges split at multiples of kRlcdPer (the stored
+        // values are per lane); a part keeps > kRlcLeaf / 2 records
+        const uint64_t al = R.distinct ? kRlcdPer : 1;
+        auto cut = [&](uint64_t q) { return q == fan ? w.second : w.first + (len * q / fan) / al * al; };
+        for (uint64_t q = 0; q < fan; q++) parts.push_back({cut(q), cut(q + 1)});
       }
       level.clear();
       if (!parts.empty()) {

@@ -36,6 +36,11 @@ enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
 // segment; a bucket of cnt entries is summed in chunks of msm_chunk(cnt)
 // entries (at least 64, at most 32 chunks), one work item per chunk
 #define CESS_MSM_SEG_BUCKETS 4096u
+// records per lane of the distinct-key RLC's Miller values (k_miller_rr): a
+// lane's value is the product of its records' Miller values
+#ifndef CESS_RLCD_PER
+#define CESS_RLCD_PER 4
+#endif
 #define CESS_MSM_MAX_SEGS 256u    // segments of one bucket pass (bucket tables <= 1 M entries, ~190 MB)
 // Segments of one bucket pass (kernel argument): parts (perm-position ranges;
 // their signatures) are segments 0 .. nparts - 1, terms (part x key group

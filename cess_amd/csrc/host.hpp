@@ -39,6 +39,8 @@ __global__ void k_codes_bitmap(uint64_t, const uint8_t*, uint64_t*);
 // RLC batch mode (k_rlc.hip)
 __global__ void k_rlc_scale(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                             uint64_t, uint32_t*, uint32_t*, uint64_t, uint64_t, uint32_t);
+__global__ void k_rlcd_scale(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                            uint64_t, uint32_t*, uint32_t*, uint64_t, uint64_t);
 __global__ void k_gt_prod(uint32_t, const uint8_t*, uint4*, uint8_t*);
 __global__ void k_g1_sum_segs(uint32_t, const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*, uint64_t,
                               uint32_t*, uint64_t);

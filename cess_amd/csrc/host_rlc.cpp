@@ -365,14 +365,14 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 
 // ---- distinct-key RLC (CESS_BLS_F_RLC_DISTINCT) -------------------------------
 // Scalars: r_i = a + b lambda with 32-bit a (odd), b from the record's
-// rlc_scalar and lambda phi's eigenvalue on G1 (k_rlc_scale kwords 1,
+// rlc_scalar and lambda phi's eigenvalue on G1 (k_rlcd_scale,
 // mul_glv32): 2^63 values, so an invalid batch passes a check with
 // probability <= 2^-63 (Ethereum consensus clients batch BLS with 64-bit
 // exponents), for 32 doublings + 32 additions per point instead of the
 // 128-bit form's 128 + 64.
 // Ranges are record-index ranges [a, b) (R.perm is the identity) whose start
 // and end (unless n) are multiples of kRlcdPer.  A range's check: S_r = sum of
-// P_i = r_i sig_i (k_rlc_scale; identity for records with a code),
+// P_i = r_i sig_i (k_rlcd_scale; identity for records with a code),
 // Miller(S_r, -G2), times the product of the range's stored lane values g_k =
 // prod f_i over i in [kRlcdPer k, kRlcdPer (k + 1)), f_i = Miller(r_i H_i, pk_i)
 // (k_miller_rr; one for records with a code), then one final exponentiation.  The products run in chunk passes (kRlcdChunk values per
@@ -500,7 +500,7 @@ static int rlcd_check(cess_bls_ctx* c, RlcState& R, const std::vector<std::pair<
 }
 
 // The batch's records through the per-signature light kernels in chunks of
-// qcap, then P_i, Q_i (k_rlc_scale) and f_i = Miller(Q_i, pk_i) kept for the
+// qcap, then P_i, Q_i (k_rlcd_scale) and f_i = Miller(Q_i, pk_i) kept for the
 // whole batch; then the batch check.
 static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint64_t index_hi, uint8_t* gt_out) {
   hipStream_t s = c->stream;
@@ -561,10 +561,10 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
     hipLaunchKernelGGL(k_prepare, dim3(g), dim3(kBlock), 0, s, m, (const uint32_t*)S.pk_aff.as<uint32_t>(),
                        S.coeffs.as<uint4>(), q, code, (const uint8_t*)inf);
     // P_i = r_i sig_i, Q_i = r_i H_i (stride n), then f_i = Miller(Q_i, pk_i)
-    hipLaunchKernelGGL(k_rlc_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
+    hipLaunchKernelGGL(k_rlcd_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
                        (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
                        (const uint32_t*)R.d_seed.as<uint32_t>(), index_hi + off, R.P.as<uint32_t>() + off,
-                       R.Q.as<uint32_t>() + off, q, n, 1u);
+                       R.Q.as<uint32_t>() + off, q, n);
     if (off + m == n) {
       // the last chunk: every P_i exists now, so the batch's S sum and its
       // single-wave Miller loop run on stream2 beside this chunk's Miller loops

@@ -134,10 +134,17 @@ __device__ __forceinline__ g1p mul_glv32(const fp& px, const fp& py, uint32_t a,
   return {mul(acc.x, acc.z), acc.y, mul(sqr(acc.z), acc.z)};
 }
 
-__global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
-                                    const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
-                                    const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
-                                    uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride, uint32_t kwords) {
+// P_i = r_i sig_i, Q_i = r_i H_i (identity for records with a code or an
+// identity point).  KW = 1: r_i = a + b lambda, a = k[0] | 1, b = k[1]
+// (mul_glv32); KW = 0: the 64-bit (kwords 2) or 128-bit (kwords 4) scalar
+// (mul128_w2).  The distinct-key mode's KW = 1 is its own kernel
+// (k_rlcd_scale), so its register allocation is not that of the 128-bit ladder.
+template <int KW>
+__device__ __forceinline__ void rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                          const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
+                                          const uint32_t* __restrict__ seed, uint64_t index_base,
+                                          uint32_t* __restrict__ P, uint32_t* __restrict__ Q, uint64_t stride,
+                                          uint64_t out_stride, uint32_t kwords) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g1p p = proj_identity<fp>(), q = proj_identity<fp>();
@@ -145,7 +152,7 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   if (code[i] == 0) {
     uint32_t k[4];
     rlc_scalar(seed, index_base + i, k);
-    if (kwords == 1) {   // r_i = a + b lambda, a = k[0] | 1, b = k[1] (mul_glv32)
+    if constexpr (KW == 1) {
       const uint32_t a = k[0] | 1u, b = k[1];
       if ((fl & INF_SIG) == 0) p = mul_glv32(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), a, b);
       if ((fl & INF_PK) == 0) q = mul_glv32(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), a, b);
@@ -158,6 +165,22 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   }
   st_g1p(P, out_stride, i, p);
   st_g1p(Q, out_stride, i, q);
+}
+
+// kwords 2 or 4 (see rlc_scale)
+__global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                    const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
+                                    const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
+                                    uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride, uint32_t kwords) {
+  rlc_scale<0>(n, code, inf, sig_aff, h_aff, seed, index_base, P, Q, stride, out_stride, kwords);
+}
+
+// the distinct-key mode's multiples (mul_glv32)
+__global__ CESS_LB void k_rlcd_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+                                     const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
+                                     const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
+                                     uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride) {
+  rlc_scale<1>(n, code, inf, sig_aff, h_aff, seed, index_base, P, Q, stride, out_stride, 1u);
 }
 
 // ---- bucket (Pippenger) sums of a check --------------------------------------

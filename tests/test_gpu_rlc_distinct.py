@@ -153,3 +153,22 @@ def test_rlc_group_fe_equals_lane_fe(ctx, dctx, monkeypatch):
     one = bytes(47) + b"\x01" + bytes(576 - 48)
     assert out["group"] == out["lane"]
     assert out["group"][0] != one and out["group"][1] == one and out["group"][2] != one
+
+
+def test_rlcd_ragged_lanes_and_cuts(ctx, dctx):
+    """4,099 records (a 4,096-record launch, then 3): the last Miller lane holds
+    three records, and the bisection's cuts fall at multiples of four records
+    (k_miller_rr's lanes) inside a range of 4,099.  Forgeries at a lane's
+    second record, at the first record of a cut and in the ragged last lane get
+    code 5; every other record 0, as the per-signature path says."""
+    sigs, pks, msgs = _distinct_batch(ctx, 4099, 19)
+    bad = [1365, 2732, 4098]
+    for j in bad:
+        msgs[j] = bytes(32)
+    packed = _pack(sigs, pks, msgs)
+    codes, words, st = dctx.verify_rlc(*packed, seed=bytes([5]) * 32)
+    want = [5 if i in bad else 0 for i in range(4099)]
+    assert list(codes) == want
+    expect, ewords = ctx.verify_fixed(*packed)
+    assert codes == expect and words == ewords
+    assert st["checks"] > 1 and st["leaves"] >= 1

@@ -867,9 +867,7 @@ CESS_HD int final_exp_staged(const A& acc0, const A& acc1, const uint8_t (*prog)
 // pt(pair) yields the pair's affine G1 point; src(pair, step) its coefficients.
 // norm1: pair 1's lines are normalised to c2 = 1 as well (a distinct-key table
 // after normalize_lines); otherwise they take the general sparse product.
-// GEN0: pair 0's lines are general too (two per-record tables: the
-// distinct-key RLC's two records per lane, k_miller_rr).
-template <bool GEN0 = false, class S, class Pt, class Src, class DG = NoDiag>
+template <class S, class Pt, class Src, class DG = NoDiag>
 CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1 = false,
                                  DG* dg = nullptr) {
   set_one12(f);
@@ -889,14 +887,10 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
       if (dg) {
         if (pr) dg->template mark<0>(); else dg->template mark<2>();
       }
-      if constexpr (GEN0) {
+      if (pr && !norm1)
         mul014(f, k.c2, c1, c4);
-      } else {
-        if (pr && !norm1)
-          mul014(f, k.c2, c1, c4);
-        else
-          mul014_one(f, c1, c4);   // -G2 table (and normalised key tables): c2 = 1
-      }
+      else
+        mul014_one(f, c1, c4);   // -G2 table (and normalised key tables): c2 = 1
       CESS_MEMBAR();
       if (dg) {
         if (pr) dg->template mark<1>(); else dg->template mark<3>();
@@ -908,6 +902,31 @@ CESS_HD void miller_loop2_staged(const S& f, bool use0, bool use1, Pt&& pt, Src&
   }
   conj12(f);   // x < 0
   if (dg) dg->template mark<5>();
+}
+
+// Miller loop over up to NP pairs with general lines sharing one accumulator
+// (the distinct-key RLC's lane of records, k_miller_rr): the product of the
+// pairs' Miller values, one squaring per step for all of them.  Bit j of `use`:
+// pair j takes part; pt(j) yields its affine G1 point, src(j, step) its
+// coefficients.
+template <int NP, class S, class Pt, class Src>
+CESS_HD void miller_loopn_staged(const S& f, uint32_t use, Pt&& pt, Src&& src) {
+  set_one12(f);
+#pragma unroll 1
+  for (int s = 0; s < N_COEFFS; s++) {
+#pragma unroll 1
+    for (int j = 0; j < NP; j++) {
+      if (!((use >> j) & 1u)) continue;
+      const coeff3 k = src(j, s);
+      const g1a p = pt(j);
+      const fp2 c1 = mul_fp(k.c1, p.x), c4 = mul_fp(k.c0, p.y);
+      mul014(f, k.c2, c1, c4);
+      CESS_MEMBAR();
+    }
+    if (square_after_step(s)) sqr12(f);
+    CESS_MEMBAR();
+  }
+  conj12(f);   // x < 0
 }
 
 }  // namespace bls

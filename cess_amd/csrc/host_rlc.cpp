@@ -366,7 +366,7 @@ static int rlc_check_multi(cess_bls_ctx* c, RlcState& R, const std::vector<std::
 // ---- distinct-key RLC (CESS_BLS_F_RLC_DISTINCT) -------------------------------
 // Scalars: r_i = a + b lambda with 32-bit a (odd), b from the record's
 // rlc_scalar and lambda phi's eigenvalue on G1 (k_rlcd_scale,
-// mul_glv32): 2^63 values, so an invalid batch passes a check with
+// g1_mul_glv32): 2^63 values, so an invalid batch passes a check with
 // probability <= 2^-63 (Ethereum consensus clients batch BLS with 64-bit
 // exponents), for 32 doublings + 32 additions per point instead of the
 // 128-bit form's 128 + 64.

@@ -42,31 +42,23 @@ __device__ __forceinline__ void miller_rr(uint64_t np, uint64_t m, const uint8_t
   }
   LdsF12 f{F, wave_first_thread()};
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  set_one12(f);
-#pragma unroll 1
-  for (int s = 0; s < N_COEFFS; s++) {
-#pragma unroll 1
-    for (int j = 0; j < RPL; j++) {
-      if (!((use >> j) & 1u)) continue;
-      const uint32_t r = RPL * k + j;
-      // each record's rows are read once: non-temporal loads (k_miller); the
-      // G1 point is re-read per line (L2), as k_miller's
-      coeff3 c;
-      uint32_t* w = &c.c0.c0.v[0];
+  const uint32_t r0 = RPL * k;
+  // the G1 point is re-read per line (L2), as k_miller's; each record's
+  // coefficient rows are read once: non-temporal loads (k_miller)
+  auto pt = [&](int j) {
+    return g1a{ld_fp(h_aff, stride, r0 + j), ld_fp(h_aff + 12 * stride, stride, r0 + j), false};
+  };
+  auto src = [&](int j, int s) {
+    coeff3 c;
+    uint32_t* w = &c.c0.c0.v[0];
 #pragma unroll
-      for (int q = 0; q < 18; q++) {
-        const u4v x = __builtin_nontemporal_load((const u4v*)(coeffs + (uint64_t)(18 * s + q) * stride + r));
-        w[4 * q] = x.x, w[4 * q + 1] = x.y, w[4 * q + 2] = x.z, w[4 * q + 3] = x.w;
-      }
-      const fp px = ld_fp(h_aff, stride, r), py = ld_fp(h_aff + 12 * stride, stride, r);
-      const fp2 c1 = mul_fp(c.c1, px), c4 = mul_fp(c.c0, py);
-      mul014(f, c.c2, c1, c4);
-      CESS_MEMBAR();
+    for (int q = 0; q < 18; q++) {
+      const u4v x = __builtin_nontemporal_load((const u4v*)(coeffs + (uint64_t)(18 * s + q) * stride + r0 + j));
+      w[4 * q] = x.x, w[4 * q + 1] = x.y, w[4 * q + 2] = x.z, w[4 * q + 3] = x.w;
     }
-    if (square_after_step(s)) sqr12(f);
-    CESS_MEMBAR();
-  }
-  conj12(f);   // x < 0
+    return c;
+  };
+  miller_loopn_staged<RPL>(f, use, pt, src);
   copy12(out, f);
 }
 

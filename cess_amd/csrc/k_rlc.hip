@@ -89,54 +89,11 @@ __device__ __forceinline__ g1p mul128_w2(const fp& px, const fp& py, const uint3
   return acc;
 }
 
-// [a + b lambda]P for 32-bit a, b, where lambda is the eigenvalue of
-// phi(x, y) = (beta x, y) on G1 (curve.hpp: phi = [-x^2]): 2-bit joint
-// windows over the affine table {P, 2P, 3P} (one inversion) and its phi image
-// (beta times the selected x): 32 doublings + 32 mixed additions, against 64 +
-// 32 for a 64-bit scalar.  The distinct-key RLC mode's scalars (2^63 values:
-// soundness 2^-63 per check).
-// Jacobian coordinates with the incomplete dbl-2009-l / madd-2007-bl
-// (curve.hpp jac_*: 2M + 5S and 7M + 4S against 6M + 2S and 12M complete) and
-// the identity tracked by a flag: P is in G1 (order r, not the identity), and
-// no step adds +-T to T.  Before the a-digit addition the accumulator is
-// [4 (A - B x^2)]P (A, B < 2^32 the digits so far, lambda = -x^2 mod r), and it
-// adds [d]P, d in 1..3: 4 (A - B x^2) = +-d has no integer solution (|both|
-// << r); before the b-digit addition it is [A' - 4 B x^2]P (A' < 2^34) and it
-// adds [-d x^2]P: A' = (4 B -+ d) x^2 needs 4 B = +-d or A' >= x^2, neither
-// possible -- so only the identity (no digit yet) is exceptional.
-__device__ __forceinline__ g1p mul_glv32(const fp& px, const fp& py, uint32_t a, uint32_t b) {
-  const g1p P2 = proj_dbl(g1p{px, py, fp_one()});
-  const g1p P3 = proj_add_mixed(P2, px, py);
-  const fp zi = inv(mul(P2.z, P3.z));
-  const fp z2i = mul(zi, P3.z), z3i = mul(zi, P2.z);
-  const fp x2 = mul(P2.x, z2i), y2 = mul(P2.y, z2i), x3 = mul(P3.x, z3i), y3 = mul(P3.y, z3i);
-  const fp beta = fp_from(c::G1_BETA);
-  g1p acc = {fp_zero(), fp_one(), fp_zero()};
-  bool id = true;
-#pragma unroll 1
-  for (int bp = 30; bp >= 0; bp -= 2) {
-    acc = jac_dbl(jac_dbl(acc));
-#pragma unroll 1
-    for (int h = 0; h < 2; h++) {
-      const uint32_t d = ((h ? b : a) >> bp) & 3u;
-      fp tx = select(d == 1, px, select(d == 2, x2, x3));
-      const fp ty = select(d == 1, py, select(d == 2, y2, y3));
-      if (h) tx = mul(tx, beta);
-      const g1p sum = jac_add_mixed(acc, tx, ty);
-      const bool take = d != 0;
-      acc = {select(take, select(id, tx, sum.x), acc.x), select(take, select(id, ty, sum.y), acc.y),
-             select(take, select(id, fp_one(), sum.z), acc.z)};
-      id = id && !take;
-    }
-  }
-  if (id) return proj_identity<fp>();
-  // Jacobian -> homogeneous (x = X / Z^2 = X Z / Z^3, y = Y / Z^3)
-  return {mul(acc.x, acc.z), acc.y, mul(sqr(acc.z), acc.z)};
-}
+// mul_glv32: curve.hpp g1_mul_glv32 (the distinct-key RLC's multiples)
 
 // P_i = r_i sig_i, Q_i = r_i H_i (identity for records with a code or an
 // identity point).  KW = 1: r_i = a + b lambda, a = k[0] | 1, b = k[1]
-// (mul_glv32); KW = 0: the 64-bit (kwords 2) or 128-bit (kwords 4) scalar
+// (g1_mul_glv32); KW = 0: the 64-bit (kwords 2) or 128-bit (kwords 4) scalar
 // (mul128_w2).  The distinct-key mode's KW = 1 is its own kernel
 // (k_rlcd_scale), so its register allocation is not that of the 128-bit ladder.
 template <int KW>
@@ -154,8 +111,8 @@ __device__ __forceinline__ void rlc_scale(uint64_t n, const uint8_t* __restrict_
     rlc_scalar(seed, index_base + i, k);
     if constexpr (KW == 1) {
       const uint32_t a = k[0] | 1u, b = k[1];
-      if ((fl & INF_SIG) == 0) p = mul_glv32(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), a, b);
-      if ((fl & INF_PK) == 0) q = mul_glv32(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), a, b);
+      if ((fl & INF_SIG) == 0) p = g1_mul_glv32(ld_fp(sig_aff, stride, i), ld_fp(sig_aff + 12 * stride, stride, i), a, b);
+      if ((fl & INF_PK) == 0) q = g1_mul_glv32(ld_fp(h_aff, stride, i), ld_fp(h_aff + 12 * stride, stride, i), a, b);
     } else {
       const int kw = kwords == 2 ? 2 : 4;
       if (kw == 2) k[2] = k[3] = 0;
@@ -175,7 +132,7 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
   rlc_scale<0>(n, code, inf, sig_aff, h_aff, seed, index_base, P, Q, stride, out_stride, kwords);
 }
 
-// the distinct-key mode's multiples (mul_glv32)
+// the distinct-key mode's multiples (g1_mul_glv32)
 __global__ CESS_LB void k_rlcd_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
                                      const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
                                      const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,

@@ -68,6 +68,14 @@ void emu_g1_mul_glv(const uint32_t* x, const uint32_t* y, const uint32_t* k, uin
   store_raw(r.x, out);
   store_raw(r.y, out + 12);
 }
+// [a + b lambda]P by curve.hpp g1_mul_glv32 (the distinct-key RLC's ladder:
+// Jacobian, incomplete formulas, affine window table) for a raw affine P of G1
+void emu_g1_mul_glv32(const uint32_t* x, const uint32_t* y, uint32_t a, uint32_t b, uint32_t* out, int* inf) {
+  g1a r = proj_to_affine(g1_mul_glv32(to_mont(load_raw(x)), to_mont(load_raw(y)), a, b));
+  *inf = r.inf;
+  store_raw(r.x, out);
+  store_raw(r.y, out + 12);
+}
 void emu_fp_inv(const uint32_t* a, uint32_t* out) { store_raw(inv(to_mont(load_raw(a))), out); }
 // safegcd inverse of a Montgomery-domain value in [0, 2p); out canonical Montgomery
 void emu_fp_inv_mont(const uint32_t* a, uint32_t* out) {
@@ -213,6 +221,37 @@ int emu_miller_pp_matches(const uint8_t* sig, const uint8_t* msg, uint32_t mlen,
                                 [](int pair) { return pts[pair]; },
                                 [](int pair, int i) { return pair ? pkc[i] : g_neg_g2[i]; });
   return eq(f1, w ? fb : fa) ? 1 : 0;
+}
+
+// The distinct-key RLC's lane loop (staged.hpp miller_loopn_staged, k_miller_rr)
+// over up to four records (H(m_j), pk_j) with the records of `use` taking part,
+// against the product of the records' single-pair loops (miller_loop2_staged
+// with pair 0 off, as k_miller runs one record).  1 equal, 0 not, -1 a key
+// does not decode.  msgs: 32 bytes each; pks: 96 bytes each.
+int emu_miller_rr_matches(const uint8_t* msgs, const uint8_t* pks, int nrec, uint32_t use) {
+  static coeff3 tab[4][N_COEFFS];
+  static g1a pts[4];
+  for (int j = 0; j < nrec; j++) {
+    uint32_t wp[24];
+    be_words(pks + 96 * j, 24, wp);
+    g2a q;
+    if (!g2_decompress(wp, q) || q.inf) return -1;
+    pts[j] = hash_to_g1(msgs + 32 * j, 32);
+    g2_prepare(q.x, q.y, [&](int i, const coeff3& k) { tab[j][i] = k; });
+  }
+  static fp12 lane, prod, one;
+  miller_loopn_staged<4>(ArrF12{&lane}, use, [](int j) { return pts[j]; },
+                         [](int j, int i) { return tab[j][i]; });
+  set_one12(ArrF12{&prod});
+  for (int j = 0; j < nrec; j++) {
+    if (!((use >> j) & 1u)) continue;
+    static int jj;
+    jj = j;
+    miller_loop2_staged(ArrF12{&one}, false, true, [](int) { return pts[jj]; },
+                        [](int, int i) { return tab[jj][i]; });
+    mul12(ArrF12{&prod}, ArrF12{&one});
+  }
+  return eq(lane, prod) ? 1 : 0;
 }
 
 // G2 key acceptance two ways: 1 accept, 0 reject, 2 identity.

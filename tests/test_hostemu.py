@@ -115,6 +115,48 @@ def test_g1_mul_glv(emu):
             assert inf.value == 0 and got == want, hex(k)
 
 
+def test_g1_mul_glv32(emu):
+    """curve.hpp g1_mul_glv32 (the distinct-key RLC's multiples r = a + b
+    lambda, lambda = -x^2 the eigenvalue of phi(x, y) = (beta x, y)): Jacobian
+    ladder with incomplete formulas over an affine table equals the oracle's
+    [a - b x^2]P, at the digit edges (leading zero windows, a = 1, b = 0,
+    all-ones digits) and on random 32-bit a (odd, as the mode draws them), b."""
+    import random
+
+    import oracle.bls_oracle as o
+    rng = random.Random(37)
+    limbs = lambda v: (ctypes.c_uint32 * 12)(*[(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+    ab = [(1, 0), (3, 0), (1, 1), (3, 3), (0xFFFFFFFF, 0xFFFFFFFF), (1, 0xFFFFFFFF), (0xFFFFFFFF, 0),
+          (0x80000001, 0x40000000), (5, 2)]
+    ab += [(rng.getrandbits(32) | 1, rng.getrandbits(32)) for _ in range(10)]
+    for j, (a, b) in enumerate(ab):
+        pt = o.ec_mul(o.FP, o.G1_GEN, rng.randrange(1, o.R)) if j % 2 else o.G1_GEN
+        out = (ctypes.c_uint32 * 24)()
+        inf = ctypes.c_int()
+        emu.emu_g1_mul_glv32(limbs(pt[0]), limbs(pt[1]), a, b, out, ctypes.byref(inf))
+        want = o.ec_mul(o.FP, pt, (a - b * o.X * o.X) % o.R)
+        got = (sum(out[i] << (32 * i) for i in range(12)), sum(out[12 + i] << (32 * i) for i in range(12)))
+        assert inf.value == 0 and got == want, (hex(a), hex(b))
+
+
+def test_miller_lane_of_records(emu, vectors):
+    """staged.hpp miller_loopn_staged (k_miller_rr: four records per lane, one
+    squaring per step for all, general lines for each) equals the product of
+    the records' single-pair Miller loops, with every record taking part and
+    with some left out (a record with a code or an identity point)."""
+    import random
+    rng = random.Random(41)
+    keys = [bytes.fromhex(c["pk"]) for c in vectors["cases"] if c["code"] == 0]
+    keys = list(dict.fromkeys(keys))[:4]
+    assert len(keys) >= 2
+    while len(keys) < 4:
+        keys.append(keys[len(keys) % 2])
+    msgs = b"".join(rng.randbytes(32) for _ in range(4))
+    pks = b"".join(keys)
+    for use in (0b1111, 0b0101, 0b1000, 0b0110):
+        assert emu.emu_miller_rr_matches(msgs, pks, 4, use) == 1, bin(use)
+
+
 def test_staged_matches_valuebased(emu, vectors):
     """The staged Fp12 code (LDS/HBM stores, final-exponentiation program) gives
     the same Gt as the value-based Fp12 code on every golden record."""

@@ -671,8 +671,8 @@ def run_rlc(args, ctx, rank, world):
         total = n * world * args.steps
         if distinct:
             what = (f"BASELINE config[1] shape through the distinct-key RLC mode (CESS_BLS_F_RLC_DISTINCT): {n} sigs per "
-                    f"GPU, {n} distinct keys, {args.forged_count} forged per GPU, one Miller value per record, one final "
-                    f"exponentiation per check, bisection over the stored Miller values")
+                    f"GPU, {n} distinct keys, {args.forged_count} forged per GPU, one pairing per record, four records per "
+                    f"Miller lane, one final exponentiation per check, bisection over the stored lane values")
         else:
             what = (f"BASELINE config[3] shape: {n} sigs per GPU, {args.keys} distinct keys, "
                     f"{args.forged_count} forged per GPU, RLC + Gt-partial RCCL all-gather + bisection")
@@ -683,7 +683,8 @@ def run_rlc(args, ctx, rank, world):
             "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: random keys (distinct)" if distinct else "synthetic: few random keys, 32-byte msgs",
             "config": {"workload": what,
-                       "timing": "host-buffer API incl. key dedup and PCIe", "parallelism": f"shard-by-index x{world}"},
+                       "timing": "host-buffer API incl. PCIe" + ("" if distinct else " and key dedup"),
+                       "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
             "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
             "runtime": runtime_provenance(),

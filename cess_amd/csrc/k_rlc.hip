@@ -133,7 +133,12 @@ __global__ CESS_LB void k_rlc_scale(uint64_t n, const uint8_t* __restrict__ code
 }
 
 // the distinct-key mode's multiples (g1_mul_glv32)
-__global__ CESS_LB void k_rlcd_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
+#if defined(CESS_RLCD_SCALE_W1)   // one wave per SIMD: 512 registers, no scratch (sweep)
+#define CESS_RLCD_SCALE_LB __launch_bounds__(256, 1)
+#else
+#define CESS_RLCD_SCALE_LB CESS_LB
+#endif
+__global__ CESS_RLCD_SCALE_LB void k_rlcd_scale(uint64_t n, const uint8_t* __restrict__ code, const uint8_t* __restrict__ inf,
                                      const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ h_aff,
                                      const uint32_t* __restrict__ seed, uint64_t index_base, uint32_t* __restrict__ P,
                                      uint32_t* __restrict__ Q, uint64_t stride, uint64_t out_stride) {

@@ -243,9 +243,12 @@ def lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
-# resident waves per SIMD of the two Fp12 kernels, fixed by their LDS images
-# (k_miller 144 KiB per block, k_final 72 KiB)
-WAVES_PER_SIMD = {"k_miller": 1, "k_final": 2}
+# resident waves per SIMD of the two Fp12 kernels, fixed by their LDS images:
+# the Miller stage runs k_miller2 (a lane pair per signature, 72 KiB per
+# 128-signature block, two blocks per CU) unless CESS_BLS_MILLER=lane selects
+# the one-lane k_miller (144 KiB per block, one wave per SIMD); k_final 72 KiB
+# 
+WAVES_PER_SIMD = {"k_miller": 1 if os.environ.get("CESS_BLS_MILLER") == "lane" else 2, "k_final": 2}
 
 
 def load_opcount():
@@ -719,7 +722,16 @@ def main():
         # one GPU per rank: fewer visible devices than ranks (or a local rank
         # past them) fails every rank at once, before any context or
         # communicator exists
-        ndev = int(os.environ.get("CESS_BENCH_DEVICE_COUNT", lib.cess_bls_device_count()))
+        # (the env override first: the library is asked only without it, and a
+        # library without the symbol -- an older build in an A/B sweep -- falls
+        # back to the KFD topology count the launcher parent uses)
+        env_n = os.environ.get("CESS_BENCH_DEVICE_COUNT")
+        if env_n is not None:
+            ndev = int(env_n)
+        elif hasattr(lib, "cess_bls_device_count"):
+            ndev = int(lib.cess_bls_device_count())
+        else:
+            ndev = node_gpu_count()
         if ndev < world or local >= ndev:
             fail("devices", 4, need=world, visible=ndev, rank=rank, local_rank=local, where="rank")
 

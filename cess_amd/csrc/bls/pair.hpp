@@ -1,0 +1,334 @@
+// Lane-pair (component-split) Fp2 arithmetic: TWO lanes per signature, lane h
+// of the pair (h = lane & 1) holds component h of every Fp2 value.
+//
+// Why (MI355X, k_miller): the one-lane Miller loop keeps its Fp12
+// accumulator in a 144 KiB LDS image of 256 signatures and needs ~490
+// registers, so it runs ONE wave per SIMD (VALU-active 0.77, 5.29 cycles per
+// instruction; profiles/round5_ax_pmc_stall.txt).  Splitting every Fp2 value
+// over a lane pair keeps the same 144 KiB image for the same 256 signatures
+// but with 512 lanes (two waves per SIMD), and halves the registers every
+// held Fp2 / Fp6 intermediate needs.
+//
+// The split follows the lazily reduced schoolbook Fp2 product (field.hpp
+// mul_scaled): component 0 of a b is a0 b0 + a1 (K - b1), component 1 is
+// a0 b1 + a1 b0 -- each ONE Montgomery reduction over two half-products, so
+// the pair does exactly the one-lane product's mads, half per lane.  A lane
+// unpacks only its own components into 28-bit digits and takes the partner's
+// digits with DPP quad-permutes (v_mov_b32_dpp, no LDS): for lane h,
+//   xa = own a digits, xb = partner's a digits (swap),
+//   ya = b0 digits (broadcast from the even lane),
+//   yb = b1 digits (broadcast from the odd lane), K - b1 on the even lane,
+// and component h = sum xa[i] ya[j] + xb[i] yb[j] (lane 0: a0 b0 + a1 (K - b1),
+// lane 1: a1 b0 + a0 b1).  Additions and subtractions are per component, so
+// each lane does half of them; multiplication by xi = 1 + u needs the partner's
+// component (own - partner on the even lane, own + partner on the odd one).
+//
+// Every condition that steers control flow must be the same in both lanes of a
+// pair (per signature): DPP reads the partner's register at the instant of the
+// instruction, so both lanes have to execute it.
+//
+// Reference: bls12_381 0.7.1's Fp2/Fp6/Fp12 arithmetic under
+// MillerLoopResult / multi_miller_loop, called at
+// utils/verify-bls-signatures/src/lib.rs:90-93.
+#pragma once
+#include "staged.hpp"
+
+#if !defined(CESS_HOSTEMU)
+namespace bls {
+
+// --- lane-pair exchange ------------------------------------------------------
+// quad_perm controls: swap [1,0,3,2], even broadcast [0,0,2,2], odd [1,1,3,3]
+// (bound_ctrl with full row/bank masks: no 'old' operand, so no v_mov
+// initialising the destination before each v_mov_b32_dpp)
+CESS_HD uint32_t dpp_swap(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true); }
+CESS_HD uint32_t dpp_even(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, true); }
+CESS_HD uint32_t dpp_odd(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, true); }
+
+// all ones on the odd lane of a pair (component 1), zero on the even lane
+CESS_HD uint32_t pair_hi_mask() { return 0u - (__lane_id() & 1u); }
+
+// the lane's component of an Fp2 value
+struct fph {
+  fp v;
+};
+struct fp6h {
+  fph c0, c1, c2;
+};
+
+CESS_HD fph fph_of(const fp& v) { return {v}; }
+CESS_HD fph add(const fph& a, const fph& b) { return {add(a.v, b.v)}; }
+CESS_HD fph sub(const fph& a, const fph& b) { return {sub(a.v, b.v)}; }
+CESS_HD fph add_nr(const fph& a, const fph& b) { return {add_nr(a.v, b.v)}; }
+CESS_HD fph dbl(const fph& a) { return {dbl(a.v)}; }
+CESS_HD fph neg(const fph& a) { return {neg(a.v)}; }
+CESS_HD fp xchg(const fp& a) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = dpp_swap(a.v[i]);
+  return r;
+}
+// * xi = 1 + u: (a0 - a1) + (a0 + a1) u -- own - partner on the even lane,
+// own + partner on the odd lane
+CESS_HD fph mul_nr(const fph& a) {
+  const fp p = xchg(a.v);
+  const fp np = neg(p);
+  const uint32_t hm = pair_hi_mask();
+  fp q;
+#pragma unroll
+  for (int i = 0; i < 12; i++) q.v[i] = (p.v[i] & hm) | (np.v[i] & ~hm);
+  return {add(a.v, q)};
+}
+// the pair's Fp2 value (1, 0) / (0, 0)
+CESS_HD fph fph_one() {
+  const uint32_t hm = pair_hi_mask();
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = c::ONE[i] & ~hm;
+  return {r};
+}
+CESS_HD fph fph_zero() { return {fp_zero()}; }
+// conjugate: the odd lane negates
+CESS_HD fph conj(const fph& a) {
+  const fp n = neg(a.v);
+  const uint32_t hm = pair_hi_mask();
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = (n.v[i] & hm) | (a.v.v[i] & ~hm);
+  return {r};
+}
+
+// digit vectors of one Fp2 operand pair (x = a, y = b) for this lane's
+// component: xa own a, xb partner's a, ya = b0, yb = b1 (odd lane) or K - b1
+// (even lane)
+CESS_HD void pair_digits(const fp& a, const fp& b, uint32_t (&xa)[14], uint32_t (&xb)[14], uint32_t (&ya)[14],
+                         uint32_t (&yb)[14]) {
+  uint32_t yo[14];
+  unpack28(a, xa);
+  unpack28(b, yo);
+  const uint32_t hm = pair_hi_mask();
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    xb[i] = dpp_swap(xa[i]);
+    ya[i] = dpp_even(yo[i]);
+    const uint32_t t = dpp_odd(yo[i]);
+    yb[i] = (t & hm) | ((c::NEG_K28[i] - t) & ~hm);
+  }
+}
+
+// this lane's component of a * b (a, b: the pair's Fp2 values, inputs < 8p as
+// mul(fp2, fp2)); result < 2p
+CESS_HD fph pmul(const fph& a0, const fph& b0) {
+  CESS_COUNT_MUL2();
+  fp a = a0.v, b = b0.v;
+  seq(a);
+  seq(b);
+  uint32_t xa[14], xb[14], ya[14], yb[14];
+  pair_digits(a, b, xa, xb, ya, yb);
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
+      mac(acc, xa[i], ya[j]);
+      mac(acc, xb[i], yb[j]);
+    }
+  });
+  seq(r);
+  return {r};
+}
+
+// this lane's component of a b + c d (one reduction; bounds as dot2)
+CESS_HD fph pdot2(const fph& a0, const fph& b0, const fph& c0, const fph& d0) {
+  CESS_COUNT_HALVES(8);
+  fp a = a0.v, b = b0.v, c = c0.v, d = d0.v;
+  seq(a);
+  seq(b);
+  seq(c);
+  seq(d);
+  uint32_t xa[14], xb[14], ya[14], yb[14], ua[14], ub[14], wa[14], wb[14];
+  pair_digits(a, b, xa, xb, ya, yb);
+  pair_digits(c, d, ua, ub, wa, wb);
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
+      mac(acc, xa[i], ya[j]);
+      mac(acc, xb[i], yb[j]);
+      mac(acc, ua[i], wa[j]);
+      mac(acc, ub[i], wb[j]);
+    }
+  });
+  seq(r);
+  return {r};
+}
+
+// a * s for s in Fp (both lanes hold s): one Fp product per lane
+CESS_HD fph pmul_fp(const fph& a, const fp& s) { return {mul(a.v, s)}; }
+
+// --- Fp6 over lane pairs ------------------------------------------------------
+CESS_HD fp6h add(const fp6h& a, const fp6h& b) { return {add(a.c0, b.c0), add(a.c1, b.c1), add(a.c2, b.c2)}; }
+CESS_HD fp6h sub(const fp6h& a, const fp6h& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1), sub(a.c2, b.c2)}; }
+CESS_HD fp6h dbl(const fp6h& a) { return {dbl(a.c0), dbl(a.c1), dbl(a.c2)}; }
+CESS_HD fp6h add_nr(const fp6h& a, const fp6h& b) {
+  return {add_nr(a.c0, b.c0), add_nr(a.c1, b.c1), add_nr(a.c2, b.c2)};
+}
+CESS_HD fp6h mul_v(const fp6h& a) { return {mul_nr(a.c2), a.c0, a.c1}; }
+
+// Karatsuba Fp6 product (as field.hpp mul(fp6, fp6))
+CESS_HD fp6h pmul6(const fp6h& a, const fp6h& b) {
+  const fph t0 = pmul(a.c0, b.c0);
+  const fph t1 = pmul(a.c1, b.c1);
+  const fph t2 = pmul(a.c2, b.c2);
+  const fph c0 = add(mul_nr(sub(sub(pmul(add_nr(a.c1, a.c2), add_nr(b.c1, b.c2)), t1), t2)), t0);
+  const fph c1 = add(sub(sub(pmul(add_nr(a.c0, a.c1), add_nr(b.c0, b.c1)), t0), t1), mul_nr(t2));
+  const fph c2 = add(sub(sub(pmul(add_nr(a.c0, a.c2), add_nr(b.c0, b.c2)), t0), t2), t1);
+  return {c0, c1, c2};
+}
+// a * (b1 v)
+CESS_HD fp6h pmul_by_1(const fp6h& a, const fph& b1) {
+  const fph p2 = pmul(a.c2, b1);
+  CESS_MEMBAR();
+  const fph p0 = pmul(a.c0, b1);
+  CESS_MEMBAR();
+  return {mul_nr(p2), p0, pmul(a.c1, b1)};
+}
+
+// One signature's Fp12 in the lane pair's LDS image G[18][256]: lane t owns
+// column t (signature t / 2, component t & 1), row 3k + q holds words
+// 4q..4q+3 of its component of coefficient k (store index as staged.hpp).
+// Conflict-free ds_read_b128 as LdsF12; t = w0 + lane id, w0 uniform.
+struct LdsPair {
+  uint4 (*G)[256];
+  uint32_t w0;
+  CESS_HD fph ld(int k) const {
+    const uint32_t t = w0 + lane_fresh();
+    fph r;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const uint4 x = G[3 * k + q][t];
+      r.v.v[4 * q] = x.x, r.v.v[4 * q + 1] = x.y, r.v.v[4 * q + 2] = x.z, r.v.v[4 * q + 3] = x.w;
+    }
+    return r;
+  }
+  CESS_HD void st(int k, const fph& a) const {
+    const uint32_t t = w0 + lane_fresh();
+#pragma unroll
+    for (int q = 0; q < 3; q++) G[3 * k + q][t] = make_uint4(a.v.v[4 * q], a.v.v[4 * q + 1], a.v.v[4 * q + 2], a.v.v[4 * q + 3]);
+  }
+};
+
+template <class S>
+CESS_HD fp6h pld6(const S& s, int h) {
+  return {s.ld(3 * h), s.ld(3 * h + 1), s.ld(3 * h + 2)};
+}
+template <class S>
+CESS_HD void pst6(const S& s, int h, const fp6h& a) {
+  s.st(3 * h, a.c0);
+  s.st(3 * h + 1, a.c1);
+  s.st(3 * h + 2, a.c2);
+}
+
+// f <- f^2 (complex squaring: 2 Fp6 products), staged.hpp sqr12
+template <class S>
+CESS_HD void psqr12(const S& f) {
+  fp6h ab;
+  {
+    const fp6h a0 = pld6(f, 0), a1 = pld6(f, 1);
+    ab = pmul6(a0, a1);
+  }
+  CESS_MEMBAR();
+  fp6h x;
+  {
+    const fp6h a0 = pld6(f, 0), a1 = pld6(f, 1);
+    x = pmul6(add_nr(a0, a1), add_nr(a0, mul_v(a1)));
+  }
+  pst6(f, 0, sub(sub(x, ab), mul_v(ab)));
+  pst6(f, 1, dbl(ab));
+}
+
+// a * (b0 + b1 v) for the Fp6 in store half h, as staged.hpp mul_by_01_dot
+template <class S>
+CESS_HD fp6h pmul_by_01_dot(const S& f, int h, const fph& b0, const fph& b1, const fph& xb1) {
+  fp6h r;
+  r.c0 = pdot2(f.ld(3 * h), b0, f.ld(3 * h + 2), xb1);
+  CESS_MEMBAR();
+  r.c1 = pdot2(f.ld(3 * h), b1, f.ld(3 * h + 1), b0);
+  CESS_MEMBAR();
+  r.c2 = pdot2(f.ld(3 * h + 1), b1, f.ld(3 * h + 2), b0);
+  return r;
+}
+
+// f <- f * (c0 + c1 v + c4 v w), staged.hpp mul014
+template <class S>
+CESS_HD void pmul014(const S& f, const fph& c0, const fph& c1, const fph& c4) {
+  const fp6h bb = pmul_by_1(pld6(f, 1), c4);
+  CESS_MEMBAR();
+  const fp6h aa = pmul_by_01_dot(f, 0, c0, c1, mul_nr(c1));
+  CESS_MEMBAR();
+  pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));   // f.c1 <- a0 + a1 (consumed below)
+  pst6(f, 0, add(mul_v(bb), aa));
+  const fp6h u = add(aa, bb);
+  CESS_MEMBAR();
+  const fph d = add(c1, c4);
+  const fp6h t = pmul_by_01_dot(f, 1, c0, d, mul_nr(d));
+  pst6(f, 1, sub(t, u));
+}
+
+// a * (1 + b1 v)
+CESS_HD fp6h pmul_by_01_one(const fp6h& a, const fph& b1) {
+  const fph p2 = pmul(a.c2, b1);
+  CESS_MEMBAR();
+  const fph p0 = pmul(a.c0, b1);
+  CESS_MEMBAR();
+  return {add(a.c0, mul_nr(p2)), add(a.c1, p0), add(a.c2, pmul(a.c1, b1))};
+}
+
+// f <- f * (1 + c1 v + c4 v w), staged.hpp mul014_one
+template <class S>
+CESS_HD void pmul014_one(const S& f, const fph& c1, const fph& c4) {
+  const fp6h bb = pmul_by_1(pld6(f, 1), c4);
+  CESS_MEMBAR();
+  const fp6h aa = pmul_by_01_one(pld6(f, 0), c1);
+  CESS_MEMBAR();
+  pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));
+  pst6(f, 0, add(mul_v(bb), aa));
+  const fp6h u = add(aa, bb);
+  CESS_MEMBAR();
+  const fp6h t = pmul_by_01_one(pld6(f, 1), add(c1, c4));
+  pst6(f, 1, sub(t, u));
+}
+
+// The two-pair Miller loop of staged.hpp miller_loop2_staged over a lane
+// pair: pt(pair) the pair's affine G1 point (both lanes), src(pair, step, c1,
+// c2, c4): this lane's components of the line's (c0, c1, c2) coefficients.
+template <class S, class Pt, class Src>
+CESS_HD void miller_loop2_pair(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1) {
+  f.st(0, fph_one());
+#pragma unroll 1
+  for (int k = 1; k < 6; k++) f.st(k, fph_zero());
+#pragma unroll 1
+  for (int s = 0; s < N_COEFFS; s++) {
+#pragma unroll 1
+    for (int pair = 0; pair < 2; pair++) {
+      const int pr = 1 - pair;
+      if (!(pr ? use1 : use0)) continue;
+      fph k0, k1, k2;
+      src(pr, s, k0, k1, k2);
+      const g1a p = pt(pr);
+      const fph c1 = pmul_fp(k1, p.x), c4 = pmul_fp(k0, p.y);
+      if (pr && !norm1)
+        pmul014(f, k2, c1, c4);
+      else
+        pmul014_one(f, c1, c4);
+      CESS_MEMBAR();
+    }
+    if (square_after_step(s)) psqr12(f);
+    CESS_MEMBAR();
+  }
+#pragma unroll 1
+  for (int k = 3; k < 6; k++) f.st(k, neg(f.ld(k)));   // conj: x < 0
+}
+
+}  // namespace bls
+#endif

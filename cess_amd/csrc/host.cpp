@@ -9,6 +9,7 @@
 #include "host.hpp"
 
 #include <stdlib.h>
+#include <string.h>
 
 #include "bls/consts.hpp"
 
@@ -117,6 +118,26 @@ static uint64_t small_records() {
   if (const char* e = getenv("CESS_BLS_SMALL_BATCH")) v = strtoull(e, nullptr, 10);
   return v;
 }
+
+// The Miller loop kernel: k_miller2 (default: a lane pair per signature,
+// 256-thread blocks of 128 signatures, two waves per SIMD; bls/pair.hpp) or
+// k_miller (one lane per signature, one wave per SIMD), env CESS_BLS_MILLER =
+// lane.  Both take the same arguments and write the same fval rows; k_miller2
+// runs config[1]'s Miller loop in 129.8-130.0 ms per 1 M against 149.5-149.7
+// (same box, profiles/round6_c_sweep_miller_pair.txt).
+typedef void (*MillerKernel)(uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint32_t*,
+                             const uint32_t*, const uint4*, uint4*, uint4*, uint64_t, const uint32_t*, uint64_t,
+                             const uint8_t*);
+static bool miller_pair() {
+  static const bool v = [] {
+    const char* e = getenv("CESS_BLS_MILLER");
+    return !(e && strcmp(e, "lane") == 0);
+  }();
+  return v;
+}
+static MillerKernel miller_kernel() { return miller_pair() ? k_miller2 : k_miller; }
+// k_miller2: 256-thread blocks of 128 signatures (a lane pair each)
+static dim3 miller_grid(uint64_t m) { return dim3(miller_pair() ? (unsigned)((m + 127) / 128) : grid_for(m)); }
 
 int cess_multi_create(const cess_bls_config* cfg, int ndev, cess_bls_ctx* c);   // host_multi.cpp
 
@@ -352,7 +373,7 @@ int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8
   };
   auto heavy = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m) -> int {
     const unsigned g = grid_for(m);
-    LAUNCH(ST_MILLER, s, k_miller, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
+    LAUNCH(ST_MILLER, s, miller_kernel(), miller_grid(m), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
            (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
            (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
            (const uint4*)S.coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q,
@@ -637,7 +658,7 @@ static int run_chunk_keyed(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uin
   };
   auto heavy = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m) -> int {
     const unsigned g = grid_for(m);
-    LAUNCH(ST_MILLER, s, k_miller, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
+    LAUNCH(ST_MILLER, s, miller_kernel(), miller_grid(m), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
            (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
            (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
            (const uint4*)c->key_coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q, idx + off,

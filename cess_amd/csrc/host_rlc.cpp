@@ -565,16 +565,9 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
                        (const uint32_t*)S.sig_aff.as<uint32_t>(), (const uint32_t*)S.h_aff.as<uint32_t>(),
                        (const uint32_t*)R.d_seed.as<uint32_t>(), index_hi + off, R.P.as<uint32_t>() + off,
                        R.Q.as<uint32_t>() + off, q, n);
-    if (off + m == n) {
-      // the last chunk: every P_i exists now, so the batch's S sum and its
-      // single-wave Miller loop run on stream2 beside this chunk's Miller loops
-      HIPCHK(hipEventRecord(c->ev_start, s));
-      HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
-      R.checks += 1;
-      r = rlcd_s_part(c, R, {{0, n}}, c->stream2);
-      if (r) return r;
-      HIPCHK(hipEventRecord(c->ev_light[0], c->stream2));
-    }
+    // the last chunk: every P_i exists once this k_rlcd_scale is done
+    const bool last = off + m == n;
+    if (last) HIPCHK(hipEventRecord(c->ev_start, s));
     hipLaunchKernelGGL(k_rlcd_records, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
                        (const uint32_t*)(R.Q.as<uint32_t>() + off), n, R.rec_h.as<uint32_t>(), R.rec_inf.as<uint8_t>(),
                        q);
@@ -585,6 +578,17 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
                        (const uint4*)S.coeffs.as<uint4>(), R.d_rec_f.as<uint4>() + off / kRlcdPer, q,
                        (n + kRlcdPer - 1) / kRlcdPer);
     HIPCHK(hipGetLastError());
+    if (last) {
+      // the batch's S sum and its single-wave Miller loop on stream2, after
+      // this chunk's k_rlcd_scale (ev_start): this chunk's k_rlcd_records and
+      // k_miller_rr are already enqueued on s, so they run beside it even
+      // though rlc_sums blocks the host until its segment table is consumed
+      HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+      R.checks += 1;
+      r = rlcd_s_part(c, R, {{0, n}}, c->stream2);
+      if (r) return r;
+      HIPCHK(hipEventRecord(c->ev_light[0], c->stream2));
+    }
     HIPCHK(hipMemcpyAsync(&R.codes[off], code, m, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));   // rebased is reused by the next chunk
   }

@@ -1,0 +1,80 @@
+// k_miller2: the two-pair Miller loop (multi_miller_loop, src/lib.rs:90-93,
+// SURVEY §8(a) A12) on a lane PAIR per signature (bls/pair.hpp): 256-thread
+// blocks of 128 signatures with the accumulator image G[18][256] (72 KiB, the
+// same bytes per signature as k_miller's F[36][256]), two blocks per CU, so
+// two waves per SIMD.  (One 512-thread block per CU measured the same waves
+// alive only ~80 % of the block's time: the older wave of a SIMD issues first
+// and finishes first, and the younger then runs alone until the block ends;
+// with two independent blocks a finished block is replaced at once.)
+// Same arguments and output (fval rows) as k_miller (k_pairing.hip), so
+// k_final and the keyed path consume it unchanged.
+#include <hip/hip_runtime.h>
+#include "soa.hpp"
+#include "bls/pair.hpp"
+
+using namespace bls;
+using namespace cess;
+
+__global__ __launch_bounds__(256, 2) void k_miller2(uint64_t n, const uint8_t* __restrict__ code,
+                                                    const uint8_t* __restrict__ inf,
+                                                    const uint32_t* __restrict__ sig_aff,
+                                                    const uint32_t* __restrict__ h_aff,
+                                                    const uint32_t* __restrict__ neg_g2,
+                                                    const uint4* __restrict__ coeffs, uint4* __restrict__ fout,
+                                                    uint4* __restrict__ pp, uint64_t stride,
+                                                    const uint32_t* __restrict__ cidx, uint64_t cstride,
+                                                    const uint8_t* __restrict__ cnorm) {
+  // signature of the pair; both lanes of a pair take every branch together
+  const uint32_t i = blockIdx.x * (blockDim.x >> 1) + (threadIdx.x >> 1);
+  if (i >= n) return;
+  if (code[i] != 0) return;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t cj = cidx ? cidx[i] : i;
+  const uint8_t fl = inf[i];
+  __shared__ uint4 G[18][256];
+  LdsPair f{G, wave_first_thread()};
+  auto pt = [&](int pair) {
+    const uint32_t* b = pair ? h_aff : sig_aff;
+    return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
+  };
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  // this lane's component of line coefficient j: rows 18k + 6j + 3h .. + 2
+  auto ld_row = [&](const uint4* base, uint64_t st, uint32_t col, int k, int j, bool nt) {
+    fph r;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const uint4* a = base + (uint64_t)(18 * k + 6 * j + 3 * h + q) * st + col;
+      u4v x;
+      if (nt)
+        x = __builtin_nontemporal_load((const u4v*)a);
+      else
+        x = *(const u4v*)a;
+      r.v.v[4 * q] = x.x, r.v.v[4 * q + 1] = x.y, r.v.v[4 * q + 2] = x.z, r.v.v[4 * q + 3] = x.w;
+    }
+    return r;
+  };
+  const uint4* g2tab = (const uint4*)neg_g2;   // 72 dwords = 18 uint4 per line, stride 1
+  auto src = [&](int pair, int k, fph& k0, fph& k1, fph& k2) {
+    if (pair) {
+      const bool nt = cidx == nullptr;
+      k0 = ld_row(coeffs, cstride, cj, k, 0, nt);
+      k1 = ld_row(coeffs, cstride, cj, k, 1, nt);
+      k2 = ld_row(coeffs, cstride, cj, k, 2, nt);
+    } else {
+      // -G2 table normalised to c2 = 1: c0 and c1 only
+      k0 = ld_row(g2tab, 1, 0, k, 0, false);
+      k1 = ld_row(g2tab, 1, 0, k, 1, false);
+    }
+  };
+  const bool norm1 = cnorm && cnorm[cj];
+  miller_loop2_pair(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1);
+  // this lane's rows of the GlobF12 output: 6k + 3h + q
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) {
+    const fph v = f.ld(k);
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+      fout[(uint64_t)(6 * k + 3 * h + q) * stride + i] =
+          make_uint4(v.v.v[4 * q], v.v.v[4 * q + 1], v.v.v[4 * q + 2], v.v.v[4 * q + 3]);
+  }
+}

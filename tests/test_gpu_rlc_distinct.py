@@ -70,7 +70,9 @@ def test_rlcd_gt_independent_of_launch_chunking(ctx, dctx):
     property of the batch and the seed alone: the same with 4,096-record
     launches (three chunks, the S sum overlapped with the last chunk) as with
     one launch, and not one for a batch with a forgery.  (The mode's scalars
-    are 64-bit, so its Gt differs from the key-grouped mode's 128-bit one.)"""
+    r = a + b*lambda take 2^63 values -- soundness 2^-63 per check, as
+    include/cess_bls.h states -- so its Gt differs from the key-grouped mode's,
+    whose scalars are 128-bit.)"""
     from cess_amd import bls
     sigs, pks, msgs = _distinct_batch(ctx, 9000, 16)
     msgs[700] = bytes(32)

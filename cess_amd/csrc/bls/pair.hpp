@@ -67,17 +67,37 @@ CESS_HD fp xchg(const fp& a) {
   for (int i = 0; i < 12; i++) r.v[i] = dpp_swap(a.v[i]);
   return r;
 }
-// * xi = 1 + u: (a0 - a1) + (a0 + a1) u -- own - partner on the even lane,
-// own + partner on the odd lane
-CESS_HD fph mul_nr(const fph& a) {
-  const fp p = xchg(a.v);
-  const fp np = neg(p);
+// the partner's component, negated (2p - x, in [0, 2p]) on the even lane:
+// lane 0 gets -a1, lane 1 gets +a0 -- the second term of xi a and of x + xi y
+CESS_HD fp partner_signed(const fp& own) {
+  const fp p = xchg(own);
   const uint32_t hm = pair_hi_mask();
-  fp q;
+  fp r;
+  uint32_t bw = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) q.v[i] = (p.v[i] & hm) | (np.v[i] & ~hm);
-  return {add(a.v, q)};
+  for (int i = 0; i < 12; i++) {
+    const uint32_t n = subc32(c::P2_RAW[i], p.v[i], bw, &bw);
+    r.v[i] = (p.v[i] & hm) | (n & ~hm);
+  }
+  return r;
 }
+// * xi = 1 + u: (a0 - a1) + (a0 + a1) u -- own - partner on the even lane,
+// own + partner on the odd lane (a summand of 2p, for a1 = 0, is removed by
+// add's conditional subtraction)
+CESS_HD fph mul_nr(const fph& a) { return {add(a.v, partner_signed(a.v))}; }
+// xi a unreduced (< 4p): for products only
+CESS_HD fph mul_nr_nr(const fph& a) { return {add_nr(a.v, partner_signed(a.v))}; }
+// a + xi b unreduced (< 6p), field.hpp add_xi_nr: for products only
+CESS_HD fph add_xi_nr(const fph& a, const fph& b) { return {add_nr(add_nr(a.v, b.v), partner_signed(b.v))}; }
+// both lanes of the pair agree on a predicate (AND of the two lanes' values)
+CESS_HD bool pair_and(bool b) {
+  const uint32_t x = b ? 1u : 0u;
+  return (x & dpp_swap(x)) != 0;
+}
+CESS_HD bool is_zero(const fph& a) { return pair_and(is_zero(a.v)); }
+CESS_HD bool eq(const fph& a, const fph& b) { return pair_and(eq(a.v, b.v)); }
+CESS_HD fph select(bool c, const fph& a, const fph& b) { return {select(c, a.v, b.v)}; }
+CESS_HD fph mul3(const fph& a) { return {mul3(a.v)}; }
 // the pair's Fp2 value (1, 0) / (0, 0)
 CESS_HD fph fph_one() {
   const uint32_t hm = pair_hi_mask();
@@ -100,6 +120,8 @@ CESS_HD fph conj(const fph& a) {
 // digit vectors of one Fp2 operand pair (x = a, y = b) for this lane's
 // component: xa own a, xb partner's a, ya = b0, yb = b1 (odd lane) or K - b1
 // (even lane)
+// (S: a's digits scaled by S <= 3 before the exchange, as mul_scaled<S>)
+template <uint32_t S = 1>
 CESS_HD void pair_digits(const fp& a, const fp& b, uint32_t (&xa)[14], uint32_t (&xb)[14], uint32_t (&ya)[14],
                          uint32_t (&yb)[14]) {
   uint32_t yo[14];
@@ -108,6 +130,7 @@ CESS_HD void pair_digits(const fp& a, const fp& b, uint32_t (&xa)[14], uint32_t 
   const uint32_t hm = pair_hi_mask();
 #pragma unroll
   for (int i = 0; i < 14; i++) {
+    if (S != 1) xa[i] *= S;
     xb[i] = dpp_swap(xa[i]);
     ya[i] = dpp_even(yo[i]);
     const uint32_t t = dpp_odd(yo[i]);
@@ -115,15 +138,17 @@ CESS_HD void pair_digits(const fp& a, const fp& b, uint32_t (&xa)[14], uint32_t 
   }
 }
 
-// this lane's component of a * b (a, b: the pair's Fp2 values, inputs < 8p as
-// mul(fp2, fp2)); result < 2p
-CESS_HD fph pmul(const fph& a0, const fph& b0) {
+// this lane's component of S a b (a, b: the pair's Fp2 values, inputs < 8p as
+// mul_scaled<S>); result < 2p
+template <uint32_t S>
+CESS_HD fph pmul_scaled(const fph& a0, const fph& b0) {
+  static_assert(S >= 1 && S <= 3, "digit bound");
   CESS_COUNT_MUL2();
   fp a = a0.v, b = b0.v;
   seq(a);
   seq(b);
   uint32_t xa[14], xb[14], ya[14], yb[14];
-  pair_digits(a, b, xa, xb, ya, yb);
+  pair_digits<S>(a, b, xa, xb, ya, yb);
   fp r = mont28([&](int k, int h, uint64_t& acc) {
 #pragma unroll
     for (int i = 0; i < 14; i++) {
@@ -135,6 +160,15 @@ CESS_HD fph pmul(const fph& a0, const fph& b0) {
   });
   seq(r);
   return {r};
+}
+CESS_HD fph pmul(const fph& a, const fph& b) { return pmul_scaled<1>(a, b); }
+
+// a^-1 in Fp2: a / (a0^2 + a1^2) conjugated (field.hpp inv(fp2)); the norm
+// and its Fp inversion are computed by both lanes
+CESS_HD fph pinv(const fph& a) {
+  const fp n = sqr(a.v);
+  const fp t = inv(add(n, xchg(n)));
+  return conj(fph{mul(a.v, t)});
 }
 
 // this lane's component of a b + c d (one reduction; bounds as dot2)

@@ -1,0 +1,356 @@
+// Final exponentiation on a lane pair per signature (MillerLoopResult::
+// final_exponentiation + Gt::is_identity, utils/verify-bls-signatures/src/
+// lib.rs:93-99): the program of staged.hpp
+// (CESS_FE_PROGRAM) with every Fp2 split over the pair as in bls/pair.hpp.
+//
+// Why: the one-lane k_final keeps its accumulators in HBM (two waves per SIMD
+// leave 288 B of LDS per lane, half an Fp12) and streams every operand of an
+// Fp12 product from there -- ~324 KB of counted traffic per signature, which
+// costs it its clock (2.13-2.20 against 2.36 GHz with the same instructions
+// on L2-resident slots, profiles/round5_v_diag_l2.txt).  A lane pair holds an
+// Fp12 in 288 B per lane, so the accumulator lives in LDS (G[18][256], 72 KiB
+// per 128-signature block, two blocks per CU) and every opcode works on it in
+// place: FE_MUL reads its slot operand once per Fp6 product (1.15 KB per
+// signature against 6.9 KB), the compressed squarings keep z2..z5 in
+// registers (48 per lane).
+#pragma once
+#include "pair.hpp"
+
+#if !defined(CESS_HOSTEMU)
+namespace bls {
+
+// One signature's Fp12 in an HBM slot (the GlobF12 rows, stride `stride`):
+// lane h reads / writes rows 6k + 3h + q of column (signature) base + lane/2.
+// `base` points at the wave's first signature (uniform); the lane part is
+// recomputed per access (staged.hpp GlobF12W).
+struct GlobPair {
+  uint4* base;
+  uint64_t stride;
+  CESS_HD uint64_t at(int k, int q) const {
+    const uint32_t l = lane_fresh();
+    return (uint64_t)(6 * k + q + 3 * (l & 1u)) * stride + (l >> 1);
+  }
+  CESS_HD fph ld(int k) const {
+    fph r;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const uint4 x = base[at(k, q)];
+      r.v.v[4 * q] = x.x, r.v.v[4 * q + 1] = x.y, r.v.v[4 * q + 2] = x.z, r.v.v[4 * q + 3] = x.w;
+    }
+    return r;
+  }
+  CESS_HD void st(int k, const fph& a) const {
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+      base[at(k, q)] = make_uint4(a.v.v[4 * q], a.v.v[4 * q + 1], a.v.v[4 * q + 2], a.v.v[4 * q + 3]);
+  }
+};
+
+template <class D, class S>
+CESS_HD void pcopy12(const D& d, const S& s) {
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) d.st(k, s.ld(k));
+}
+template <class S>
+CESS_HD void pconj12(const S& f) {
+#pragma unroll 1
+  for (int k = 3; k < 6; k++) f.st(k, neg(f.ld(k)));
+}
+// f == 1, the same answer in both lanes
+template <class S>
+CESS_HD bool pis_one12(const S& f) {
+  bool r = eq(f.ld(0).v, fph_one().v);
+#pragma unroll 1
+  for (int k = 1; k < 6; k++) r = r && is_zero(f.ld(k).v);
+  return pair_and(r);
+}
+// a == conj(b) (a b == 1 for b cyclotomic), the same answer in both lanes
+template <class A, class B>
+CESS_HD bool pis_conj12(const A& a, const B& b) {
+  bool r = true;
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r = r && eq(a.ld(k).v, k < 3 ? b.ld(k).v : neg(b.ld(k).v));
+  return pair_and(r);
+}
+
+// Karatsuba Fp6 product with the first operand fetched per use (a(j): this
+// lane's component of coefficient j, e.g. an LDS load or a sum of two) and
+// the second held in registers
+template <class LA>
+CESS_HD fp6h pmul6_lr(LA&& a, const fp6h& b) {
+  const fph v0 = pmul(a(0), b.c0);
+  CESS_MEMBAR();
+  const fph v1 = pmul(a(1), b.c1);
+  CESS_MEMBAR();
+  const fph v2 = pmul(a(2), b.c2);
+  CESS_MEMBAR();
+  const fph c0 = add(mul_nr(sub(sub(pmul(add_nr(a(1), a(2)), add_nr(b.c1, b.c2)), v1), v2)), v0);
+  CESS_MEMBAR();
+  const fph c1 = add(sub(sub(pmul(add_nr(a(0), a(1)), add_nr(b.c0, b.c1)), v0), v1), mul_nr(v2));
+  CESS_MEMBAR();
+  const fph c2 = add(sub(sub(pmul(add_nr(a(0), a(2)), add_nr(b.c0, b.c2)), v0), v2), v1);
+  return {c0, c1, c2};
+}
+
+// f <- f g in place (f: the LDS accumulator, g: a slot), Karatsuba over Fp6
+// ordered so that at most one Fp6 product is held: t0 = f0 g0;
+// x = (f0 + f1)(g0 + g1); f0 <- x - t0 (f0 is dead: t1 needs f1 only);
+// t1 = f1 g1; f1 <- f0 - t1 = f0 g1 + f1 g0; f0 <- t0 + v t1.
+template <class S, class G>
+CESS_HD void pmul12(const S& f, const G& g) {
+  fp6h t0;
+  {
+    const fp6h g0 = pld6(g, 0);
+    t0 = pmul6_lr([&](int j) { return f.ld(j); }, g0);
+  }
+  CESS_MEMBAR();
+  {
+    fp6h gs;
+    {
+      const fp6h g0 = pld6(g, 0), g1 = pld6(g, 1);
+      gs = add_nr(g0, g1);
+    }
+    const fp6h x = pmul6_lr([&](int j) { return add_nr(f.ld(j), f.ld(3 + j)); }, gs);
+    CESS_MEMBAR();
+    pst6(f, 0, sub(x, t0));
+  }
+  CESS_MEMBAR();
+  fp6h t1;
+  {
+    const fp6h g1 = pld6(g, 1);
+    t1 = pmul6_lr([&](int j) { return f.ld(3 + j); }, g1);
+  }
+  CESS_MEMBAR();
+  pst6(f, 1, sub(pld6(f, 0), t1));
+  pst6(f, 0, add(t0, mul_v(t1)));
+}
+
+// Fp6 square of the store half h (a pmul6 of the half with itself)
+template <class S>
+CESS_HD fp6h psqr6(const S& f, int h) {
+  const fp6h a = pld6(f, h);
+  return pmul6_lr([&](int j) { return f.ld(3 * h + j); }, a);
+}
+
+// f <- f^-1 in place (staged.hpp inv12_stream): t = a0^2 - v a1^2,
+// t^-1 = (c0, c1, c2) / (t0 c0 + xi (t2 c1 + t1 c2)), f = (a0 t^-1, -a1 t^-1)
+template <class S>
+CESS_HD void pinv12(const S& f) {
+  fp6h ti;
+  {
+    fp6h t;
+    {
+      const fp6h s0 = psqr6(f, 0);
+      CESS_MEMBAR();
+      t = sub(s0, mul_v(psqr6(f, 1)));
+    }
+    CESS_MEMBAR();
+    const fph c0 = sub(pmul(t.c0, t.c0), mul_nr(pmul(t.c1, t.c2)));
+    CESS_MEMBAR();
+    const fph c1 = sub(mul_nr(pmul(t.c2, t.c2)), pmul(t.c0, t.c1));
+    CESS_MEMBAR();
+    const fph c2 = sub(pmul(t.c1, t.c1), pmul(t.c0, t.c2));
+    CESS_MEMBAR();
+    const fph den = add(pmul(t.c0, c0), mul_nr(pdot2(t.c2, c1, t.c1, c2)));
+    const fph di = pinv(den);
+    CESS_MEMBAR();
+    ti = {pmul(c0, di), pmul(c1, di), pmul(c2, di)};
+  }
+  CESS_MEMBAR();
+  pst6(f, 0, pmul6_lr([&](int j) { return f.ld(j); }, ti));
+  CESS_MEMBAR();
+  const fp6h r1 = pmul6_lr([&](int j) { return f.ld(3 + j); }, ti);
+  pst6(f, 1, {neg(r1.c0), neg(r1.c1), neg(r1.c2)});
+}
+
+// the lane's component of the Frobenius constant gamma_{k,i} (field.hpp frob_coeff)
+CESS_HD fph pfrob_coeff(int k, int i) {
+  const uint32_t hm = pair_hi_mask();
+  fp r;
+#pragma unroll
+  for (int w = 0; w < 12; w++) r.v[w] = (c::FROB[k - 1][i][1][w] & hm) | (c::FROB[k - 1][i][0][w] & ~hm);
+  return {r};
+}
+// f <- f^(p^k) in place (staged.hpp frob12)
+template <class S>
+CESS_HD void pfrob12(const S& f, int k) {
+#pragma unroll 1
+  for (int s = 0; s < 6; s++) {
+    const int i = (s % 3) * 2 + s / 3;
+    fph y = f.ld(s);
+    if (k & 1) y = conj(y);
+    if (i) y = pmul(y, pfrob_coeff(k, i));
+    f.st(s, y);
+  }
+}
+
+// (a + b s)^2 in Fp4 (field.hpp fp4_square)
+CESS_HD void pfp4_square(fph& c0, fph& c1, const fph& a, const fph& b) {
+  const fph t0 = pmul(a, a);
+  CESS_MEMBAR();
+  const fph t1 = pmul(b, b);
+  CESS_MEMBAR();
+  c0 = add(mul_nr(t1), t0);
+  const fph s = add_nr(a, b);
+  c1 = sub(sub(pmul(s, s), t0), t1);
+}
+// n Granger-Scott cyclotomic squarings of the store f (staged.hpp
+// cyc_square_run / cycsq12), the six coefficients in registers (72 per lane)
+template <class S>
+CESS_HD void pcyc_square_run(const S& f, int n) {
+  fph z[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) z[k] = f.ld(k);
+#pragma unroll 1
+  for (int r = 0; r < n; r++) {
+    CESS_MEMBAR();
+    fph t0, t1;
+    pfp4_square(t0, t1, z[0], z[4]);
+    z[0] = add(dbl(sub(t0, z[0])), t0);
+    z[4] = add(dbl(add(t1, z[4])), t1);
+    CESS_MEMBAR();
+    fph t2, t3;
+    pfp4_square(t0, t1, z[3], z[2]);
+    CESS_MEMBAR();
+    pfp4_square(t2, t3, z[1], z[5]);
+    z[1] = add(dbl(sub(t0, z[1])), t0);
+    z[5] = add(dbl(add(t1, z[5])), t1);
+    const fph n3 = mul_nr(t3);
+    z[3] = add(dbl(add(n3, z[3])), n3);
+    z[2] = add(dbl(sub(t2, z[2])), t2);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) f.st(k, z[k]);
+}
+
+// n Karabina compressed squarings (staged.hpp kcyc_run) of (z2, z3, z4, z5),
+// all in registers
+CESS_HD void pkcyc_run(fph& z2, fph& z3, fph& z4, fph& z5, int n) {
+#pragma unroll 1
+  for (int r = 0; r < n; r++) {
+    CESS_MEMBAR();
+    fph u, v;
+    {
+      const fph b3 = pmul_scaled<3>(z4, z5);
+      CESS_MEMBAR();
+      const fph t3 = pmul_scaled<3>(add_nr(z4, z5), add_xi_nr(z4, z5));
+      const fph nb3 = mul_nr(b3);
+      u = sub(sub(t3, b3), nb3);   // 3 (z4^2 + xi z5^2)
+      v = dbl(nb3);                // 6 xi z4 z5
+    }
+    CESS_MEMBAR();
+    {
+      const fph b3 = pmul_scaled<3>(z2, z3);
+      CESS_MEMBAR();
+      const fph t3 = pmul_scaled<3>(add_nr(z2, z3), add_xi_nr(z2, z3));
+      z4 = sub(sub(sub(t3, b3), mul_nr(b3)), dbl(z4));
+      z5 = dbl(add(z5, b3));
+    }
+    CESS_MEMBAR();
+    z2 = add(dbl(z2), v);
+    z3 = sub(u, dbl(z3));
+  }
+}
+
+// staged.hpp cyc_z1_frac / cyc_z1_den / cyc_z0
+CESS_HD void pcyc_z1_frac(const fph& z2, const fph& z3, const fph& z4, const fph& z5, fph& num, fph& den) {
+  if (is_zero(z2)) {   // pair-uniform, practically never taken
+    num = dbl(pmul(z4, z5));
+    den = z3;
+  } else {
+    num = sub(add(mul_nr(pmul(z5, z5)), mul3(pmul(z4, z4))), dbl(z3));
+    den = dbl(dbl(z2));
+  }
+}
+CESS_HD fph pcyc_z1_den(const fph& z2, const fph& z3) { return is_zero(z2) ? z3 : dbl(dbl(z2)); }
+CESS_HD fph pcyc_z0(const fph& z1, const fph& z2, const fph& z3, const fph& z4, const fph& z5) {
+  return add(mul_nr(add(dbl(pmul(z1, z1)), pdot2(z2, z5, neg(mul3(z3)), z4))), fph_one());
+}
+
+// FE_CHAIN (staged.hpp cyc_chain): the powers a^(2^k), k = 16, 48, 57, 60, 62,
+// 63, of the cyclotomic element in `base` into the stores X(0..5)
+template <class B, class XFn>
+CESS_HD void pcyc_chain(const B& base, XFn&& X) {
+  {
+    fph z4 = base.ld(1), z5 = base.ld(5), z2 = base.ld(3), z3 = base.ld(2);
+    int k = 0;
+#pragma unroll 1
+    for (int j = 0; j < 6; j++) {
+      const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+      pkcyc_run(z2, z3, z4, z5, stop - k);
+      k = stop;
+      CESS_MEMBAR();
+      const auto x = X(j);
+      x.st(3, z2);
+      x.st(2, z3);
+      x.st(1, z4);
+      x.st(5, z5);
+    }
+  }
+  CESS_MEMBAR();
+  bool degen = false;
+  fph prod = fph_one();
+#pragma unroll 1
+  for (int j = 0; j < 6; j++) {
+    const auto x = X(j);
+    fph num, den;
+    pcyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
+    const bool z = is_zero(den);
+    degen = degen || z;
+    x.st(4, num);
+    x.st(0, prod);   // product of the denominators before j
+    prod = pmul(prod, select(z, fph_one(), den));
+    CESS_MEMBAR();
+  }
+  fph iv = pinv(prod);
+#pragma unroll 1
+  for (int j = 5; j >= 0; j--) {
+    const auto x = X(j);
+    const fph den = pcyc_z1_den(x.ld(3), x.ld(2));
+    const fph ivj = pmul(iv, x.ld(0));   // 1 / den_j
+    iv = pmul(iv, select(is_zero(den), fph_one(), den));
+    CESS_MEMBAR();
+    const fph z1 = pmul(x.ld(4), ivj);
+    x.st(4, z1);
+    CESS_MEMBAR();
+    x.st(0, pcyc_z0(z1, x.ld(3), x.ld(2), x.ld(1), x.ld(5)));
+    CESS_MEMBAR();
+  }
+  if (degen) {   // pair-uniform; Granger-Scott squarings with X(5) as the running power
+    const auto w = X(5);
+    pcopy12(w, base);
+#pragma unroll 1
+    for (int j = 0; j < 5; j++) {
+      const int run = j == 0 ? 16 : j == 1 ? 32 : j == 2 ? 9 : j == 3 ? 3 : 2;
+      pcyc_square_run(w, run);
+      pcopy12(X(j), w);
+    }
+    pcyc_square_run(w, 1);
+  }
+}
+
+// The program (staged.hpp final_exp_staged) on ONE in-place accumulator
+// (FE_MUL and FE_INV work in place here); slot(s) returns the store of slot s.
+template <class A, class SlotFn>
+CESS_HD void final_exp_pair(const A& acc, const uint8_t (*prog)[2], SlotFn&& slot) {
+#pragma unroll 1
+  for (int pc = 0;; pc++) {
+    const uint8_t op = prog[pc][0], arg = prog[pc][1];
+    if (op == FE_END) break;
+    switch (op) {
+      case FE_LOAD: pcopy12(acc, slot(arg)); break;
+      case FE_STORE: pcopy12(slot(arg), acc); break;
+      case FE_MUL: pmul12(acc, slot(arg)); break;
+      case FE_SQN: pcyc_square_run(acc, arg); break;
+      case FE_CONJ: pconj12(acc); break;
+      case FE_FROB: pfrob12(acc, arg); break;
+      case FE_INV: pinv12(acc); break;
+      case FE_CHAIN: pcyc_chain(slot(arg), [&](int j) { return slot(SL_X0 + j); }); break;
+      default: break;
+    }
+    CESS_MEMBAR();
+  }
+}
+
+}  // namespace bls
+#endif

@@ -139,6 +139,22 @@ static MillerKernel miller_kernel() { return miller_pair() ? k_miller2 : k_mille
 // k_miller2: 256-thread blocks of 128 signatures (a lane pair each)
 static dim3 miller_grid(uint64_t m) { return dim3(miller_pair() ? (unsigned)((m + 127) / 128) : grid_for(m)); }
 
+// The final-exponentiation kernel: k_final2 (default: a lane pair per
+// signature, the accumulator in LDS; bls/pair_fe.hpp) or k_final (one lane per
+// signature, accumulators in HBM), env CESS_BLS_FINAL = lane.  Same arguments
+// and outputs; k_final2 137.4-138.2 against 142.1 ms per 1 M on one box, ~99
+// against ~332 KB/sig counted traffic (profiles/round6_e_sweep_final_pair.txt).
+typedef void (*FinalKernel)(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);
+static bool final_pair() {
+  static const bool v = [] {
+    const char* e = getenv("CESS_BLS_FINAL");
+    return !(e && strcmp(e, "lane") == 0);
+  }();
+  return v;
+}
+static FinalKernel final_kernel() { return final_pair() ? k_final2 : k_final; }
+static dim3 final_grid(uint64_t m) { return dim3(final_pair() ? (unsigned)((m + 127) / 128) : grid_for(m)); }
+
 int cess_multi_create(const cess_bls_config* cfg, int ndev, cess_bls_ctx* c);   // host_multi.cpp
 
 extern "C" int cess_bls_ctx_create(const cess_bls_config* cfg, cess_bls_ctx** out) {
@@ -379,7 +395,7 @@ int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8
            (const uint4*)S.coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q,
            (const uint32_t*)nullptr, q, (const uint8_t*)nullptr);
     if (n > c->qcap) HIPCHK(hipEventRecord(c->ev_mill[(off / c->qcap) & 1], s));
-    LAUNCH(ST_FINAL, s, k_final, dim3(g), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
+    LAUNCH(ST_FINAL, s, final_kernel(), final_grid(m), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
            c->fe_slots.as<uint4>(), bitmap + off / 64, gt ? gt + 576 * off : (uint8_t*)nullptr, q);
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;
@@ -664,7 +680,7 @@ static int run_chunk_keyed(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uin
            (const uint4*)c->key_coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q, idx + off,
            (uint64_t)c->nkeys, (const uint8_t*)c->key_norm.as<uint8_t>());
     if (n > c->qcap) HIPCHK(hipEventRecord(c->ev_mill[(off / c->qcap) & 1], s));
-    LAUNCH(ST_FINAL, s, k_final, dim3(g), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
+    LAUNCH(ST_FINAL, s, final_kernel(), final_grid(m), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
            c->fe_slots.as<uint4>(), bitmap + off / 64, (uint8_t*)nullptr, q);
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;

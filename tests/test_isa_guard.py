@@ -81,6 +81,9 @@ def test_staged_kernels_scratch_budget(tmp_path):
     # the lane-pair Miller loop (bls/pair.hpp) at two waves per SIMD: 256
     # registers and a few spilled values (152 B/lane in round 6)
     assert pair[0].get(".private_segment_fixed_size", 1 << 20) <= 256, pair
+    # the lane-pair final exponentiation (bls/pair_fe.hpp): no scratch
+    final2 = [v for k, v in notes.items() if k.startswith("_Z8k_final2")]
+    assert final2 and final2[0].get(".private_segment_fixed_size", 1 << 20) <= 64, final2
     assert final[0].get(".private_segment_fixed_size", 1 << 20) <= 1024, final
     # the SSWU values parked in LDS (bls/h2c.hpp hash_to_g1_parked): k_hash and
     # k_hash_out 304 -> 24 B/lane, k_sign 512 -> 384 (its GLV ladder spills the

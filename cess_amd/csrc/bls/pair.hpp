@@ -197,6 +197,72 @@ CESS_HD fph pdot2(const fph& a0, const fph& b0, const fph& c0, const fph& d0) {
   return {r};
 }
 
+// Prepared operands: the digit vectors of pair_digits computed once for an
+// operand that several products share (each preparation is an unpack plus
+// 14-28 DPP moves and, for a y operand, the K - b1 selection).
+struct pxd {   // x side: own digits, partner's digits
+  uint32_t a[14], b[14];
+};
+struct pyd {   // y side: b0 digits, b1 (odd lane) or K - b1 (even lane) digits
+  uint32_t a[14], b[14];
+};
+CESS_HD pxd prep_x(const fph& x0) {
+  fp x = x0.v;
+  seq(x);
+  pxd r;
+  unpack28(x, r.a);
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.b[i] = dpp_swap(r.a[i]);
+  return r;
+}
+CESS_HD pyd prep_y(const fph& y0) {
+  fp y = y0.v;
+  seq(y);
+  uint32_t yo[14];
+  unpack28(y, yo);
+  const uint32_t hm = pair_hi_mask();
+  pyd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    r.a[i] = dpp_even(yo[i]);
+    const uint32_t t = dpp_odd(yo[i]);
+    r.b[i] = (t & hm) | ((c::NEG_K28[i] - t) & ~hm);
+  }
+  return r;
+}
+// this lane's component of x y / x y + u w from prepared operands (bounds as
+// pmul / pdot2)
+CESS_HD fph pmul_p(const pxd& x, const pyd& y) {
+  CESS_COUNT_MUL2();
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
+      mac(acc, x.a[i], y.a[j]);
+      mac(acc, x.b[i], y.b[j]);
+    }
+  });
+  seq(r);
+  return {r};
+}
+CESS_HD fph pdot2_p(const pxd& x, const pyd& y, const pxd& u, const pyd& w) {
+  CESS_COUNT_HALVES(8);
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
+      mac(acc, x.a[i], y.a[j]);
+      mac(acc, x.b[i], y.b[j]);
+      mac(acc, u.a[i], w.a[j]);
+      mac(acc, u.b[i], w.b[j]);
+    }
+  });
+  seq(r);
+  return {r};
+}
+
 // a * s for s in Fp (both lanes hold s): one Fp product per lane
 CESS_HD fph pmul_fp(const fph& a, const fp& s) { return {mul(a.v, s)}; }
 
@@ -220,12 +286,24 @@ CESS_HD fp6h pmul6(const fp6h& a, const fp6h& b) {
   return {c0, c1, c2};
 }
 // a * (b1 v)
+#ifndef CESS_PAIR_PREP
+#define CESS_PAIR_PREP 1
+#endif
 CESS_HD fp6h pmul_by_1(const fp6h& a, const fph& b1) {
+#if CESS_PAIR_PREP
+  const pyd y = prep_y(b1);   // shared by the three products
+  const fph p2 = pmul_p(prep_x(a.c2), y);
+  CESS_MEMBAR();
+  const fph p0 = pmul_p(prep_x(a.c0), y);
+  CESS_MEMBAR();
+  return {mul_nr(p2), p0, pmul_p(prep_x(a.c1), y)};
+#else
   const fph p2 = pmul(a.c2, b1);
   CESS_MEMBAR();
   const fph p0 = pmul(a.c0, b1);
   CESS_MEMBAR();
   return {mul_nr(p2), p0, pmul(a.c1, b1)};
+#endif
 }
 
 // One signature's Fp12 in the lane pair's LDS image G[18][256]: lane t owns
@@ -284,6 +362,20 @@ CESS_HD void psqr12(const S& f) {
 // a * (b0 + b1 v) for the Fp6 in store half h, as staged.hpp mul_by_01_dot
 template <class S>
 CESS_HD fp6h pmul_by_01_dot(const S& f, int h, const fph& b0, const fph& b1, const fph& xb1) {
+#if CESS_PAIR_PREP
+  // b0 enters all three dot products, b1 two, each coefficient of f two
+  const pyd y0 = prep_y(b0);
+  fp6h r;
+  {
+    const pxd x0 = prep_x(f.ld(3 * h));
+    r.c0 = pdot2_p(x0, y0, prep_x(f.ld(3 * h + 2)), prep_y(xb1));
+    CESS_MEMBAR();
+    r.c1 = pdot2_p(x0, prep_y(b1), prep_x(f.ld(3 * h + 1)), y0);
+  }
+  CESS_MEMBAR();
+  r.c2 = pdot2_p(prep_x(f.ld(3 * h + 1)), prep_y(b1), prep_x(f.ld(3 * h + 2)), y0);
+  return r;
+#else
   fp6h r;
   r.c0 = pdot2(f.ld(3 * h), b0, f.ld(3 * h + 2), xb1);
   CESS_MEMBAR();
@@ -291,6 +383,7 @@ CESS_HD fp6h pmul_by_01_dot(const S& f, int h, const fph& b0, const fph& b1, con
   CESS_MEMBAR();
   r.c2 = pdot2(f.ld(3 * h + 1), b1, f.ld(3 * h + 2), b0);
   return r;
+#endif
 }
 
 // f <- f * (c0 + c1 v + c4 v w), staged.hpp mul014
@@ -298,24 +391,33 @@ template <class S>
 CESS_HD void pmul014(const S& f, const fph& c0, const fph& c1, const fph& c4) {
   const fp6h bb = pmul_by_1(pld6(f, 1), c4);
   CESS_MEMBAR();
-  const fp6h aa = pmul_by_01_dot(f, 0, c0, c1, mul_nr(c1));
+  const fp6h aa = pmul_by_01_dot(f, 0, c0, c1, mul_nr_nr(c1));
   CESS_MEMBAR();
   pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));   // f.c1 <- a0 + a1 (consumed below)
   pst6(f, 0, add(mul_v(bb), aa));
   const fp6h u = add(aa, bb);
   CESS_MEMBAR();
   const fph d = add(c1, c4);
-  const fp6h t = pmul_by_01_dot(f, 1, c0, d, mul_nr(d));
+  const fp6h t = pmul_by_01_dot(f, 1, c0, d, mul_nr_nr(d));
   pst6(f, 1, sub(t, u));
 }
 
 // a * (1 + b1 v)
 CESS_HD fp6h pmul_by_01_one(const fp6h& a, const fph& b1) {
+#if CESS_PAIR_PREP
+  const pyd y = prep_y(b1);   // shared by the three products
+  const fph p2 = pmul_p(prep_x(a.c2), y);
+  CESS_MEMBAR();
+  const fph p0 = pmul_p(prep_x(a.c0), y);
+  CESS_MEMBAR();
+  return {add(a.c0, mul_nr(p2)), add(a.c1, p0), add(a.c2, pmul_p(prep_x(a.c1), y))};
+#else
   const fph p2 = pmul(a.c2, b1);
   CESS_MEMBAR();
   const fph p0 = pmul(a.c0, b1);
   CESS_MEMBAR();
   return {add(a.c0, mul_nr(p2)), add(a.c1, p0), add(a.c2, pmul(a.c1, b1))};
+#endif
 }
 
 // f <- f * (1 + c1 v + c4 v w), staged.hpp mul014_one

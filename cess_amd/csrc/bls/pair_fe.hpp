@@ -44,6 +44,28 @@ struct GlobPair {
     for (int q = 0; q < 3; q++)
       base[at(k, q)] = make_uint4(a.v.v[4 * q], a.v.v[4 * q + 1], a.v.v[4 * q + 2], a.v.v[4 * q + 3]);
   }
+  // both components of coefficient k (k may differ between the two lanes)
+  CESS_HD fp2 ld_full(int k) const {
+    const uint32_t l = lane_fresh() >> 1;
+    fp2 r;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const uint4 x = base[(uint64_t)(6 * k + q) * stride + l];
+      fp& d = q < 3 ? r.c0 : r.c1;
+      const int o = 4 * (q % 3);
+      d.v[o] = x.x, d.v[o + 1] = x.y, d.v[o + 2] = x.z, d.v[o + 3] = x.w;
+    }
+    return r;
+  }
+  CESS_HD void st_full(int k, const fp2& a) const {
+    const uint32_t l = lane_fresh() >> 1;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const fp& s = q < 3 ? a.c0 : a.c1;
+      const int o = 4 * (q % 3);
+      base[(uint64_t)(6 * k + q) * stride + l] = make_uint4(s.v[o], s.v[o + 1], s.v[o + 2], s.v[o + 3]);
+    }
+  }
 };
 
 template <class D, class S>
@@ -252,6 +274,56 @@ CESS_HD void pkcyc_run(fph& z2, fph& z3, fph& z4, fph& z5, int n) {
   }
 }
 
+// 2p - a (in (0, 2p] for a in [0, 2p)): a negation for add() only
+CESS_HD fp2 neg_2p(const fp2& a) {
+  fp2 r;
+  uint32_t b0 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.v[i] = subc32(c::P2_RAW[i], a.c0.v[i], b0, &b0);
+    r.c1.v[i] = subc32(c::P2_RAW[i], a.c1.v[i], b1, &b1);
+  }
+  return r;
+}
+CESS_HD fp2 xchg2(const fp2& a) { return {xchg(a.c0), xchg(a.c1)}; }
+
+// n Karabina compressed squarings split by PRODUCTS over the pair: the
+// squaring's two halves are independent -- (z4, z5) gives 3 (z4^2 + xi z5^2)
+// and 6 xi z4 z5, which update z3 and z2; (z2, z3) gives 3 (z2^2 + xi z3^2)
+// and 6 z2 z3, which update z4 and z5 -- so lane 0 holds (u, w) = (z4, z5)
+// and lane 1 (u, w) = (z2, z3) as FULL Fp2 values, each runs its half's two
+// lazily reduced products (mul_scaled<3>, no per-product exchange) and the
+// lanes swap two Fp2 results per squaring.  Per signature ~8 % fewer VALU
+// instructions than the component-split pkcyc_run.  With A = 3 (u^2 + xi w^2),
+// b3 = 3 u w: lane 0 sends (2 xi b3, A), lane 1 sends (A, 2 b3), and with
+// (f, s) received
+//   lane 0:  z4' = f - 2 z4,  z5' = s + 2 z5
+//   lane 1:  z2' = f + 2 z2,  z3' = s - 2 z3.
+CESS_HD void pkcyc_run_ps(fp2& u, fp2& w, int n) {
+  const bool hi = pair_hi_mask() != 0;
+#pragma unroll 1
+  for (int r = 0; r < n; r++) {
+    CESS_MEMBAR();
+    fp2 f, sc;
+    {
+      const fp2 b3 = mul_scaled<3>(u, w);
+      CESS_MEMBAR();
+      const fp2 t3 = mul_scaled<3>(add_nr(u, w), add_xi_nr(u, w));
+      const fp2 nb3 = mul_nr(b3);
+      const fp2 A = sub(sub(t3, b3), nb3);
+      const fp2 D = dbl(select(hi, b3, nb3));
+      f = select(hi, A, D);
+      sc = select(hi, D, A);
+    }
+    CESS_MEMBAR();
+    f = xchg2(f);
+    sc = xchg2(sc);
+    const fp2 du = dbl(u), dw = dbl(w);
+    u = add(f, select(hi, du, neg_2p(du)));
+    w = add(sc, select(hi, neg_2p(dw), dw));
+  }
+}
+
 // staged.hpp cyc_z1_frac / cyc_z1_den / cyc_z0
 CESS_HD void pcyc_z1_frac(const fph& z2, const fph& z3, const fph& z4, const fph& z5, fph& num, fph& den) {
   if (is_zero(z2)) {   // pair-uniform, practically never taken
@@ -271,6 +343,28 @@ CESS_HD fph pcyc_z0(const fph& z1, const fph& z2, const fph& z3, const fph& z4, 
 // 63, of the cyclotomic element in `base` into the stores X(0..5)
 template <class B, class XFn>
 CESS_HD void pcyc_chain(const B& base, XFn&& X) {
+#ifndef CESS_PAIR_KCYC_PS
+#define CESS_PAIR_KCYC_PS 1
+#endif
+#if CESS_PAIR_KCYC_PS
+  {
+    // store indices of (u, w): lane 0 (z4, z5) = (1, 5), lane 1 (z2, z3) = (3, 2)
+    const bool hi = pair_hi_mask() != 0;
+    const int ku = hi ? 3 : 1, kw = hi ? 2 : 5;
+    fp2 u = base.ld_full(ku), w = base.ld_full(kw);
+    int k = 0;
+#pragma unroll 1
+    for (int j = 0; j < 6; j++) {
+      const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+      pkcyc_run_ps(u, w, stop - k);
+      k = stop;
+      CESS_MEMBAR();
+      const auto x = X(j);
+      x.st_full(ku, u);
+      x.st_full(kw, w);
+    }
+  }
+#else
   {
     fph z4 = base.ld(1), z5 = base.ld(5), z2 = base.ld(3), z3 = base.ld(2);
     int k = 0;
@@ -287,6 +381,7 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
       x.st(5, z5);
     }
   }
+#endif
   CESS_MEMBAR();
   bool degen = false;
   fph prod = fph_one();

@@ -51,12 +51,15 @@ __global__ __launch_bounds__(256, 2) void k_final2(uint64_t n, uint8_t* __restri
     }
   }
   // 32 signatures per wave: the ballot's even bits, bit (i mod 32) of the
-  // 32-bit half word i / 32 of the LSB-first bitmap
+  // 32-bit half word i / 32 of the LSB-first bitmap; every half of a 64-bit
+  // word that holds a record is written (zero bits past the last record, as
+  // k_final's whole-word ballot)
   uint64_t x = __ballot(c == 0) & 0x5555555555555555ull;
   x = (x | (x >> 1)) & 0x3333333333333333ull;
   x = (x | (x >> 2)) & 0x0f0f0f0f0f0f0f0full;
   x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
   x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
   x = (x | (x >> 16)) & 0x00000000ffffffffull;
-  if ((threadIdx.x & 63) == 0 && i < n) reinterpret_cast<uint32_t*>(bitmap)[i >> 5] = (uint32_t)x;
+  if ((threadIdx.x & 63) == 0 && n > 0 && (i >> 6) <= ((n - 1) >> 6))
+    reinterpret_cast<uint32_t*>(bitmap)[i >> 5] = (uint32_t)x;
 }

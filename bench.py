@@ -249,6 +249,10 @@ def lib_sha256() -> str:
 # the one-lane k_miller (144 KiB per block, one wave per SIMD); k_final 72 KiB
 # 
 WAVES_PER_SIMD = {"k_miller": 1 if os.environ.get("CESS_BLS_MILLER") == "lane" else 2, "k_final": 2}
+# the kernel that runs a stage (its name in the rocprofv3 PMC summaries): the
+# lane-pair kernels by default, the one-lane ones with CESS_BLS_MILLER / _FINAL = lane
+KERNEL_OF_STAGE = {"k_miller": "k_miller" if os.environ.get("CESS_BLS_MILLER") == "lane" else "k_miller2",
+                   "k_final": "k_final" if os.environ.get("CESS_BLS_FINAL") == "lane" else "k_final2"}
 
 
 def load_opcount():
@@ -621,6 +625,36 @@ def run_dry(args, rank, world):
         rdv_cleanup(rank, world)
 
 
+def rlc_roofline(ctx, stages, n, distinct):
+    """Roofline of an RLC line's dominant chunk kernel: its algorithmic mads per
+    launch (profiles/opcount.json: k_miller_rr per record in the distinct-key
+    mode, the per-signature kernels' counts otherwise) / its average HIP-event
+    launch time; HBM traffic from a committed PMC profile of this library
+    build (same SHA-256) when one exists."""
+    if not stages:
+        return None
+    oc = load_opcount()
+    dom = max(stages, key=lambda k: stages[k][0])
+    ms, launches = stages[dom]
+    chunk = min(n, ctx.launch_records)
+    if distinct and dom == "k_miller":
+        kernel, per = "k_miller_rr", oc.get("rlcd", {}).get("k_miller_rr")
+    else:
+        kernel, per = dom, oc["per_stage"].get(dom)
+    if not per or not launches:
+        return None
+    alg = (per["mul"] + per["sqr"]) * ALG_MADS_PER_FP_MUL * chunk
+    achieved = alg / (ms / launches * 1e-3)
+    sha = lib_sha256()
+    pmc = load_pmc_traffic(sha, kernel)
+    kd = (pmc or {}).get("all", {}).get(kernel) or {}
+    return {"bound": "valu-int", "kernel": kernel, "stage": dom, "achieved": achieved / 1e12,
+            "peak": PEAK_MADS / 1e12, "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
+            "frac": achieved / PEAK_MADS, "launch_ms": ms / launches, "records_per_launch": chunk,
+            "alg_mads_per_record": (per["mul"] + per["sqr"]) * ALG_MADS_PER_FP_MUL,
+            "traffic": kd.get("hbm_bytes_per_launch"), "traffic_source": pmc["_file"] if pmc else None}
+
+
 def run_rlc(args, ctx, rank, world):
     """RLC batch mode (BASELINE config[3] shape): each rank holds n records
     signed by `keys` distinct TEE keys; one combination per rank, the Gt
@@ -657,6 +691,7 @@ def run_rlc(args, ctx, rank, world):
     if world > 1:
         ctx.comm_barrier()
     ctx.synchronize()
+    ctx.stage_stats(reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         codes, words, st = step()
@@ -664,6 +699,9 @@ def run_rlc(args, ctx, rank, world):
     if world > 1:
         ctx.comm_barrier()
     elapsed = time.perf_counter() - t0
+    # HIP-event times of the chunk kernels inside the timed steps (the library
+    # records them with CESS_BLS_F_PROFILE; host_rlc.cpp RLAUNCH)
+    stages = {k: v for k, v in ctx.stage_stats(reset=True).items() if v[1] > 0}
     expect = np.zeros(n, dtype=np.uint8)
     expect[forged] = 5
     ok = bool((np.frombuffer(codes, dtype=np.uint8) == expect).all())
@@ -679,6 +717,7 @@ def run_rlc(args, ctx, rank, world):
         else:
             what = (f"BASELINE config[3] shape: {n} sigs per GPU, {args.keys} distinct keys, "
                     f"{args.forged_count} forged per GPU, RLC + Gt-partial RCCL all-gather + bisection")
+        roofline = rlc_roofline(ctx, stages, n, distinct)
         print(json.dumps({
             "metric": "verified BLS12-381 sigs/sec (node), RLC batch mode", "value": total / elapsed,
             "unit": "sigs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -690,6 +729,8 @@ def run_rlc(args, ctx, rank, world):
                        "parallelism": f"shard-by-index x{world}"},
             "verdicts_ok": ok,
             "rlc_stats": {k: (int(v) if not isinstance(v, bool) else v) for k, v in st.items()},
+            "stage_ms_per_step": {k: v[0] / args.steps for k, v in stages.items()},
+            "roofline": roofline,
             "runtime": runtime_provenance(),
         }), flush=True)
 
@@ -751,7 +792,8 @@ def main():
         ctx.close()
         return
     if args.mode in ("rlc", "rlcd"):
-        ctx = bls.Context(device=local, max_batch=min(args.n or (4 << 20), 1 << 20), rlc_distinct=args.mode == "rlcd")
+        ctx = bls.Context(device=local, max_batch=min(args.n or (4 << 20), 1 << 20), rlc_distinct=args.mode == "rlcd",
+                          profile=True)
         if world > 1:
             comm_setup(ctx, rank, world, args.transport, args.one_device)
         run_rlc(args, ctx, rank, world)
@@ -864,10 +906,11 @@ def main():
         alg = (per[dom]["mul"] + per[dom]["sqr"]) * ALG_MADS_PER_FP_MUL * chunk
         achieved = alg / (dom_ms * 1e-3)
         sha = lib_sha256()
-        pmc = load_pmc_traffic(sha, dom, chunk)
+        dom_kernel = KERNEL_OF_STAGE.get(dom, dom)
+        pmc = load_pmc_traffic(sha, dom_kernel, chunk)
         traffic = valu_active = None
         if pmc and pmc.get("n") == chunk:
-            kd = pmc.get("all", {}).get(dom) or {}
+            kd = pmc.get("all", {}).get(dom_kernel) or {}
             traffic = kd.get("hbm_bytes_per_launch")
             # the issue bound the kernels sit on: share of each wave's cycles
             # with a VALU instruction issued (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
@@ -918,7 +961,8 @@ def main():
             "bitmap_popcount": popcount,
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "stage_launches_per_step": {k: v / args.steps for k, v in launches_of.items()},
-            "roofline": {"bound": "valu-int", "kernel": dom, "achieved": achieved / 1e12, "peak": PEAK_MADS / 1e12,
+            "roofline": {"bound": "valu-int", "kernel": dom_kernel, "stage": dom, "achieved": achieved / 1e12,
+                         "peak": PEAK_MADS / 1e12,
                          "unit": "T mad/s (32x32-bit limb products, v_mad_u64_u32)",
                          "frac": achieved / PEAK_MADS, "traffic": traffic,
                          "traffic_source": pmc["_file"] if pmc else None,

@@ -12,7 +12,20 @@
 using namespace cess_host;
 
 namespace {
-constexpr uint64_t kRlcLeaf = 2048;   // records verified per signature
+constexpr uint64_t kRlcLeaf = 2048;
+
+// per-kernel HIP-event records of the RLC path's chunk kernels (with
+// CESS_BLS_F_PROFILE; host.cpp LAUNCH): bench.py's RLC lines take their
+// roofline from these (the Miller stage is k_miller_rr in the distinct-key mode)
+#define RLAUNCH(stage, strm, ...)                        \
+  do {                                                   \
+    hipEvent_t pa_;                                      \
+    int pr_ = prof_begin(c, strm, stage, &pa_);          \
+    if (pr_) return pr_;                                 \
+    hipLaunchKernelGGL(__VA_ARGS__);                     \
+    pr_ = prof_end(c, strm, stage, pa_);                 \
+    if (pr_) return pr_;                                 \
+  } while (0)   // records verified per signature
 constexpr uint64_t kRlcFan = 16;      // bisection fan-out per level
 // distinct-key mode: a level re-multiplies stored Miller values and costs one
 // single-wave Miller loop and final exponentiation of latency whatever its
@@ -552,13 +565,13 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
     const unsigned g = grid_for(m);
     // the per-signature decode / hash / prepare (run_chunk's light kernels;
     // codes in the reference's precedence)
-    hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
+    RLAUNCH(ST_DECODE_SIG, s, k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
                        code, inf, S.sig_aff.as<uint32_t>(), q);
-    hipLaunchKernelGGL(k_decode_pk, dim3(g), dim3(kBlock), 0, s, m, c->in_pks.as<uint8_t>(), (const uint8_t*)nullptr,
+    RLAUNCH(ST_DECODE_PK, s, k_decode_pk, dim3(g), dim3(kBlock), 0, s, m, c->in_pks.as<uint8_t>(), (const uint8_t*)nullptr,
                        code, inf, S.pk_aff.as<uint32_t>(), q, strict);
-    hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
+    RLAUNCH(ST_HASH, s, k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
                        (const uint8_t*)code, S.h_aff.as<uint32_t>(), q);
-    hipLaunchKernelGGL(k_prepare, dim3(g), dim3(kBlock), 0, s, m, (const uint32_t*)S.pk_aff.as<uint32_t>(),
+    RLAUNCH(ST_PREPARE, s, k_prepare, dim3(g), dim3(kBlock), 0, s, m, (const uint32_t*)S.pk_aff.as<uint32_t>(),
                        S.coeffs.as<uint4>(), q, code, (const uint8_t*)inf);
     // P_i = r_i sig_i, Q_i = r_i H_i (stride n), then f_i = Miller(Q_i, pk_i)
     hipLaunchKernelGGL(k_rlcd_scale, dim3(g), dim3(kBlock), 0, s, m, (const uint8_t*)code, (const uint8_t*)inf,
@@ -573,7 +586,7 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
                        q);
     // g_k straight into the batch-wide lane values (stride ceil(n / P))
     const uint64_t np = (m + kRlcdPer - 1) / kRlcdPer;
-    hipLaunchKernelGGL(k_miller_rr, dim3(grid_for(np)), dim3(kBlock), 0, s, np, m, (const uint8_t*)code,
+    RLAUNCH(ST_MILLER, s, k_miller_rr, dim3(grid_for(np)), dim3(kBlock), 0, s, np, m, (const uint8_t*)code,
                        (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
                        (const uint4*)S.coeffs.as<uint4>(), R.d_rec_f.as<uint4>() + off / kRlcdPer, q,
                        (n + kRlcdPer - 1) / kRlcdPer);
@@ -742,7 +755,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     uint32_t* sig_dst = R.pts ? R.Xs.as<uint32_t>() + off : S.sig_aff.as<uint32_t>();
     uint32_t* h_dst = R.pts ? R.Xh.as<uint32_t>() + off : S.h_aff.as<uint32_t>();
     const uint64_t pstride = R.pts ? n : c->qcap;
-    hipLaunchKernelGGL(k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
+    RLAUNCH(ST_DECODE_SIG, s, k_decode_sig, dim3(g), dim3(kBlock), 0, s, m, c->in_sigs.as<uint8_t>(), (const uint8_t*)nullptr,
                        c->code.as<uint8_t>(), S.inf.as<uint8_t>(), sig_dst, pstride);
     HIPCHK(hipGetLastError());
     hc.resize(m);
@@ -759,7 +772,7 @@ int cess_host::rlc_begin_at(cess_bls_ctx* c, size_t n, const uint8_t* sigs, cons
     memcpy(&R.codes[off], hc.data(), m);
     HIPCHK(hipMemcpyAsync(c->code.p, hc.data(), m, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(S.inf.p, hi.data(), m, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
+    RLAUNCH(ST_HASH, s, k_hash, dim3(g), dim3(kBlock), 0, s, m, c->in_msgs.as<uint8_t>(), c->in_offs.as<uint64_t>(),
                        (const uint8_t*)c->code.as<uint8_t>(), h_dst, pstride);
     if (R.pts) {
       HIPCHK(hipMemcpyAsync(R.d_code.as<uint8_t>() + off, hc.data(), m, hipMemcpyHostToDevice, s));
@@ -897,7 +910,9 @@ int cess_host::verify_rlc_host(cess_bls_ctx* c, size_t n, const uint8_t* sigs, c
                                uint64_t* stats4) {
   int r = rlc_begin_at(c, n, sigs, pks, msgs, offs, seed32, 0, nullptr);
   if (r) return r;
-  return rlc_finish(c, codes_out, bitmap_out, stats4);
+  r = rlc_finish(c, codes_out, bitmap_out, stats4);
+  if (r) return r;
+  return collect_profile(c, c->stream);   // no-op without CESS_BLS_F_PROFILE
 }
 
 #define ENTRY(c)                          \

@@ -254,6 +254,29 @@ int emu_miller_rr_matches(const uint8_t* msgs, const uint8_t* pks, int nrec, uin
   return eq(lane, prod) ? 1 : 0;
 }
 
+#if defined(CESS_COUNT_OPS)
+// (half-multiply, square) counts of k_miller_rr's lane loop (staged.hpp
+// miller_loopn_staged<4>) over four records (H(m_j), pk_j), all taking part:
+// the distinct-key RLC's Miller work for four records (tools/opcount.py)
+void emu_opcount_rr(const uint8_t* msgs, const uint8_t* pks, uint64_t* out) {
+  static coeff3 tab[4][N_COEFFS];
+  static g1a pts[4];
+  for (int j = 0; j < 4; j++) {
+    uint32_t wp[24];
+    be_words(pks + 96 * j, 24, wp);
+    g2a q;
+    g2_decompress(wp, q);
+    pts[j] = hash_to_g1(msgs + 32 * j, 32);
+    g2_prepare(q.x, q.y, [&](int i, const coeff3& k) { tab[j][i] = k; });
+  }
+  static fp12 lane;
+  g_mul_count = g_sqr_count = g_mul2_count = g_half_count = 0;
+  miller_loopn_staged<4>(ArrF12{&lane}, 0xFu, [](int j) { return pts[j]; }, [](int j, int i) { return tab[j][i]; });
+  out[0] = 2 * g_mul_count + 5 * g_mul2_count + g_half_count;
+  out[1] = g_sqr_count;
+}
+#endif
+
 // G2 key acceptance two ways: 1 accept, 0 reject, 2 identity.
 // split = 1: as the kernels do it -- k_decode_pk's on-curve decode, then
 // k_prepare's psi(Q) == -T check on the [|x|]Q of the G2Prepared iteration;

@@ -44,6 +44,16 @@ for g in vec["keygen_sign"]:
     srows.append((out[0] / 2, out[1]))
 res["generator"] = {"k_sign": {"mul": sum(r[0] for r in srows) / len(srows),
                                "sqr": sum(r[1] for r in srows) / len(srows), "samples": len(srows)}}
+# the distinct-key RLC's Miller lane loop (k_miller_rr, four records per lane)
+# over four valid golden records, per record
+valid = [c for c in vec["cases"] if c["code"] == 0 and len(c["msg"]) == 64 and len(c["pk"]) == 192]
+if len(valid) >= 4:
+    rr = (ctypes.c_uint64 * 2)()
+    L.emu_opcount_rr(b"".join(bytes.fromhex(c["msg"]) for c in valid[:4]),
+                     b"".join(bytes.fromhex(c["pk"]) for c in valid[:4]), rr)
+    res["rlcd"] = {"k_miller_rr": {"mul": rr[0] / 2 / 4, "sqr": rr[1] / 4, "records_per_lane": 4,
+                                   "what": "per record: one general sparse product per line and a quarter of "
+                                           "the lane's accumulator squarings"}}
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 json.dump(res, open(os.path.join(ROOT, "profiles", "opcount.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -24,3 +24,5 @@ timeout -k 10 560 bash tools/profile.sh $T 1048576 > gpurun_out/${T}_profile.log
 tail -1 gpurun_out/${T}_profile.log
 timeout -k 10 400 bash tools/pmc_stall.sh $T 262144 "k_final|k_miller" > gpurun_out/${T}_stall.log 2>&1 || { tail -5 gpurun_out/${T}_stall.log; exit 9; }
 tail -3 gpurun_out/${T}_stall.log
+timeout -k 10 600 bash tools/profile_rlcd.sh $T > gpurun_out/${T}_profile_rlcd.log 2>&1 || { tail -5 gpurun_out/${T}_profile_rlcd.log; exit 10; }
+tail -1 gpurun_out/${T}_profile_rlcd.log

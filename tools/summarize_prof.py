@@ -27,8 +27,10 @@ if stats:
 agg = {}
 for f in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        # (grid = n, or n plus the padding of a wave-padded list: k_rsa_verify_2048u)
-        if not n <= int(r["Grid_Size"]) <= n + (1 << 18):
+        # (grid = n, or n plus the padding of a wave-padded list: k_rsa_verify_2048u;
+        # the lane-pair kernels k_miller2 / k_final2 run two lanes per record: 2n)
+        g = int(r["Grid_Size"])
+        if not (n <= g <= n + (1 << 18) or 2 * n <= g <= 2 * n + 256):
             continue
         k = r["Kernel_Name"].split("(")[0]
         d = agg.setdefault(k, {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),

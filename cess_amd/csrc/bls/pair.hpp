@@ -32,6 +32,7 @@
 // utils/verify-bls-signatures/src/lib.rs:90-93.
 #pragma once
 #include "staged.hpp"
+#include "../kernels.hpp"
 
 #if !defined(CESS_HOSTEMU)
 namespace bls {
@@ -306,12 +307,12 @@ CESS_HD fp6h pmul_by_1(const fp6h& a, const fph& b1) {
 #endif
 }
 
-// One signature's Fp12 in the lane pair's LDS image G[18][256]: lane t owns
+// One signature's Fp12 in the lane pair's LDS image G[18][CESS_PAIR_THREADS]: lane t owns
 // column t (signature t / 2, component t & 1), row 3k + q holds words
 // 4q..4q+3 of its component of coefficient k (store index as staged.hpp).
 // Conflict-free ds_read_b128 as LdsF12; t = w0 + lane id, w0 uniform.
 struct LdsPair {
-  uint4 (*G)[256];
+  uint4 (*G)[CESS_PAIR_THREADS];
   uint32_t w0;
   CESS_HD fph ld(int k) const {
     const uint32_t t = w0 + lane_fresh();
@@ -457,6 +458,34 @@ CESS_HD void miller_loop2_pair(const S& f, bool use0, bool use1, Pt&& pt, Src&& 
         pmul014(f, k2, c1, c4);
       else
         pmul014_one(f, c1, c4);
+      CESS_MEMBAR();
+    }
+    if (square_after_step(s)) psqr12(f);
+    CESS_MEMBAR();
+  }
+#pragma unroll 1
+  for (int k = 3; k < 6; k++) f.st(k, neg(f.ld(k)));   // conj: x < 0
+}
+
+// Miller loop over up to NP pairs with general lines sharing one accumulator
+// (staged.hpp miller_loopn_staged, the distinct-key RLC's lane of records) on
+// a lane pair: bit j of `use` (the same in both lanes) -- pair j takes part;
+// pt(j) its affine G1 point, src(j, step, k0, k1, k2) this lane's components
+// of its line coefficients.
+template <int NP, class S, class Pt, class Src>
+CESS_HD void miller_loopn_pair(const S& f, uint32_t use, Pt&& pt, Src&& src) {
+  f.st(0, fph_one());
+#pragma unroll 1
+  for (int k = 1; k < 6; k++) f.st(k, fph_zero());
+#pragma unroll 1
+  for (int s = 0; s < N_COEFFS; s++) {
+#pragma unroll 1
+    for (int j = 0; j < NP; j++) {
+      if (!((use >> j) & 1u)) continue;
+      fph k0, k1, k2;
+      src(j, s, k0, k1, k2);
+      const g1a p = pt(j);
+      pmul014(f, k2, pmul_fp(k1, p.x), pmul_fp(k0, p.y));
       CESS_MEMBAR();
     }
     if (square_after_step(s)) psqr12(f);

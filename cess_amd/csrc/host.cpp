@@ -136,8 +136,16 @@ static bool miller_pair() {
   return v;
 }
 static MillerKernel miller_kernel() { return miller_pair() ? k_miller2 : k_miller; }
-// k_miller2: 256-thread blocks of 128 signatures (a lane pair each)
-static dim3 miller_grid(uint64_t m) { return dim3(miller_pair() ? (unsigned)((m + 127) / 128) : grid_for(m)); }
+// the lane-pair kernels: blocks of CESS_PAIR_THREADS / 2 signatures
+constexpr uint64_t kPairSigs = CESS_PAIR_THREADS / 2;
+// (covering whole 64-record bitmap words: k_final2 writes 32-bit halves, one per
+// wave of 32 signatures, so both waves of a word must exist)
+static unsigned pair_grid(uint64_t m) {
+  const uint64_t m64 = (m + 63) & ~63ull;
+  return (unsigned)((m64 + kPairSigs - 1) / kPairSigs);
+}
+static dim3 miller_grid(uint64_t m) { return dim3(miller_pair() ? pair_grid(m) : grid_for(m)); }
+static dim3 miller_block() { return dim3(miller_pair() ? CESS_PAIR_THREADS : kBlock); }
 
 // The final-exponentiation kernel: k_final2 (default: a lane pair per
 // signature, the accumulator in LDS; bls/pair_fe.hpp) or k_final (one lane per
@@ -153,7 +161,8 @@ static bool final_pair() {
   return v;
 }
 static FinalKernel final_kernel() { return final_pair() ? k_final2 : k_final; }
-static dim3 final_grid(uint64_t m) { return dim3(final_pair() ? (unsigned)((m + 127) / 128) : grid_for(m)); }
+static dim3 final_grid(uint64_t m) { return dim3(final_pair() ? pair_grid(m) : grid_for(m)); }
+static dim3 final_block() { return dim3(final_pair() ? CESS_PAIR_THREADS : kBlock); }
 
 int cess_multi_create(const cess_bls_config* cfg, int ndev, cess_bls_ctx* c);   // host_multi.cpp
 
@@ -389,13 +398,13 @@ int cess_host::run_chunk(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uint8
   };
   auto heavy = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m) -> int {
     const unsigned g = grid_for(m);
-    LAUNCH(ST_MILLER, s, miller_kernel(), miller_grid(m), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
+    LAUNCH(ST_MILLER, s, miller_kernel(), miller_grid(m), miller_block(), 0, s, m, (const uint8_t*)(codes + off),
            (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
            (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
            (const uint4*)S.coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q,
            (const uint32_t*)nullptr, q, (const uint8_t*)nullptr);
     if (n > c->qcap) HIPCHK(hipEventRecord(c->ev_mill[(off / c->qcap) & 1], s));
-    LAUNCH(ST_FINAL, s, final_kernel(), final_grid(m), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
+    LAUNCH(ST_FINAL, s, final_kernel(), final_grid(m), final_block(), 0, s, m, codes + off, c->fval.as<uint4>(),
            c->fe_slots.as<uint4>(), bitmap + off / 64, gt ? gt + 576 * off : (uint8_t*)nullptr, q);
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;
@@ -674,13 +683,13 @@ static int run_chunk_keyed(cess_bls_ctx* c, hipStream_t s, uint64_t n, const uin
   };
   auto heavy = [&](StageSlot& S, uint64_t q, uint64_t off, uint64_t m) -> int {
     const unsigned g = grid_for(m);
-    LAUNCH(ST_MILLER, s, miller_kernel(), miller_grid(m), dim3(kBlock), 0, s, m, (const uint8_t*)(codes + off),
+    LAUNCH(ST_MILLER, s, miller_kernel(), miller_grid(m), miller_block(), 0, s, m, (const uint8_t*)(codes + off),
            (const uint8_t*)S.inf.as<uint8_t>(), (const uint32_t*)S.sig_aff.as<uint32_t>(),
            (const uint32_t*)S.h_aff.as<uint32_t>(), (const uint32_t*)c->neg_g2.as<uint32_t>(),
            (const uint4*)c->key_coeffs.as<uint4>(), c->fval.as<uint4>(), c->fe_slots.as<uint4>(), q, idx + off,
            (uint64_t)c->nkeys, (const uint8_t*)c->key_norm.as<uint8_t>());
     if (n > c->qcap) HIPCHK(hipEventRecord(c->ev_mill[(off / c->qcap) & 1], s));
-    LAUNCH(ST_FINAL, s, final_kernel(), final_grid(m), dim3(kBlock), 0, s, m, codes + off, c->fval.as<uint4>(),
+    LAUNCH(ST_FINAL, s, final_kernel(), final_grid(m), final_block(), 0, s, m, codes + off, c->fval.as<uint4>(),
            c->fe_slots.as<uint4>(), bitmap + off / 64, (uint8_t*)nullptr, q);
     HIPCHK(hipGetLastError());
     return CESS_BLS_OK;

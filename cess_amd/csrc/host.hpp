@@ -28,6 +28,8 @@ __global__ void k_miller2(uint64_t, const uint8_t*, const uint8_t*, const uint32
                           const uint4*, uint4*, uint4*, uint64_t, const uint32_t*, uint64_t, const uint8_t*);
 __global__ void k_miller_rr(uint64_t, uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint4*, uint4*,
                             uint64_t, uint64_t);
+__global__ void k_miller_rr2(uint64_t, uint64_t, const uint8_t*, const uint8_t*, const uint32_t*, const uint4*, uint4*,
+                            uint64_t, uint64_t);
 __global__ void k_norm_keys(uint64_t, uint64_t, uint4*, uint32_t*, uint8_t*);
 __global__ void k_merge_pk(uint64_t, const uint32_t*, uint32_t, const uint8_t*, const uint8_t*, uint8_t*, uint8_t*);
 __global__ void k_final(uint64_t, uint8_t*, uint4*, uint4*, uint64_t*, uint8_t*, uint64_t);

@@ -3,6 +3,7 @@
 // failure the batch is bisected down to leaves of kRlcLeaf records, which are
 // verified per signature, so the final codes are those of
 // cess_bls_verify_batch (up to the 2^-127 soundness error per check).
+#include <string.h>
 #include <sys/random.h>
 
 #include <thread>
@@ -586,7 +587,12 @@ static int rlcd_begin(cess_bls_ctx* c, RlcState& R, const uint8_t* seed32, uint6
                        q);
     // g_k straight into the batch-wide lane values (stride ceil(n / P))
     const uint64_t np = (m + kRlcdPer - 1) / kRlcdPer;
-    RLAUNCH(ST_MILLER, s, k_miller_rr, dim3(grid_for(np)), dim3(kBlock), 0, s, np, m, (const uint8_t*)code,
+    // (k_miller_rr2: a lane pair per lane of records, two waves per SIMD,
+    // unless CESS_BLS_MILLER=lane selects the one-lane kernels)
+    static const bool rr_pair = !(getenv("CESS_BLS_MILLER") && strcmp(getenv("CESS_BLS_MILLER"), "lane") == 0);
+    RLAUNCH(ST_MILLER, s, rr_pair ? k_miller_rr2 : k_miller_rr,
+            dim3(rr_pair ? (unsigned)((np + CESS_PAIR_THREADS / 2 - 1) / (CESS_PAIR_THREADS / 2)) : grid_for(np)),
+            dim3(rr_pair ? CESS_PAIR_THREADS : kBlock), 0, s, np, m, (const uint8_t*)code,
                        (const uint8_t*)R.rec_inf.as<uint8_t>(), (const uint32_t*)R.rec_h.as<uint32_t>(),
                        (const uint4*)S.coeffs.as<uint4>(), R.d_rec_f.as<uint4>() + off / kRlcdPer, q,
                        (n + kRlcdPer - 1) / kRlcdPer);

@@ -16,7 +16,7 @@ using namespace cess;
 __constant__ uint8_t kFeProgramPair[][2] = {CESS_FE_PROGRAM};
 __constant__ uint8_t kFeProgramPairVerify[][2] = {CESS_FE_PROGRAM_VERIFY};
 
-__global__ __launch_bounds__(256, 2) void k_final2(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
+__global__ __launch_bounds__(CESS_PAIR_THREADS, 2) void k_final2(uint64_t n, uint8_t* __restrict__ code, uint4* __restrict__ fin,
                                                    uint4* __restrict__ slots, uint64_t* __restrict__ bitmap,
                                                    uint8_t* __restrict__ gt_out, uint64_t stride) {
   // signature of the pair; both lanes of a pair take every branch together
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256, 2) void k_final2(uint64_t n, uint8_t* __restri
     if (c == 0) {
       // slot views start at the wave's first signature (uniform)
       const uint32_t s0 = blockIdx.x * (blockDim.x >> 1) + (wave_first_thread() >> 1);
-      __shared__ uint4 G[18][256];
+      __shared__ uint4 G[18][CESS_PAIR_THREADS];
       const LdsPair acc{G, wave_first_thread()};
       auto slot = [&](int s) {
         return GlobPair{(s == SL_F ? fin : slots + (uint64_t)(s - 1) * 36 * stride) + s0, stride};

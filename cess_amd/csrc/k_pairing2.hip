@@ -15,7 +15,7 @@
 using namespace bls;
 using namespace cess;
 
-__global__ __launch_bounds__(256, 2) void k_miller2(uint64_t n, const uint8_t* __restrict__ code,
+__global__ __launch_bounds__(CESS_PAIR_THREADS, 2) void k_miller2(uint64_t n, const uint8_t* __restrict__ code,
                                                     const uint8_t* __restrict__ inf,
                                                     const uint32_t* __restrict__ sig_aff,
                                                     const uint32_t* __restrict__ h_aff,
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256, 2) void k_miller2(uint64_t n, const uint8_t* _
   const uint32_t h = threadIdx.x & 1u;
   const uint32_t cj = cidx ? cidx[i] : i;
   const uint8_t fl = inf[i];
-  __shared__ uint4 G[18][256];
+  __shared__ uint4 G[18][CESS_PAIR_THREADS];
   LdsPair f{G, wave_first_thread()};
   auto pt = [&](int pair) {
     const uint32_t* b = pair ? h_aff : sig_aff;
@@ -76,5 +76,67 @@ __global__ __launch_bounds__(256, 2) void k_miller2(uint64_t n, const uint8_t* _
     for (int q = 0; q < 3; q++)
       fout[(uint64_t)(6 * k + 3 * h + q) * stride + i] =
           make_uint4(v.v.v[4 * q], v.v.v[4 * q + 1], v.v.v[4 * q + 2], v.v.v[4 * q + 3]);
+  }
+}
+
+// k_miller_rr2: the distinct-key RLC's lane of CESS_RLCD_PER records
+// (k_pairing_rr.hip k_miller_rr: g_k = prod_j Miller(Q_i, pk_i) over records
+// i = 4k + j, src/lib.rs:90-93) on a lane pair per lane of records, as
+// k_miller2: blocks of CESS_PAIR_THREADS / 2 record lanes, the accumulator in
+// LDS, two waves per SIMD.  Same arguments and output rows as k_miller_rr.
+__global__ __launch_bounds__(CESS_PAIR_THREADS, 2) void k_miller_rr2(uint64_t np, uint64_t m,
+                                                                     const uint8_t* __restrict__ code,
+                                                                     const uint8_t* __restrict__ inf,
+                                                                     const uint32_t* __restrict__ h_aff,
+                                                                     const uint4* __restrict__ coeffs,
+                                                                     uint4* __restrict__ fout, uint64_t stride,
+                                                                     uint64_t fstride) {
+  constexpr int RPL = CESS_RLCD_PER;
+  // the lane of records k of the pair; both lanes take every branch together
+  const uint32_t k = blockIdx.x * (blockDim.x >> 1) + (threadIdx.x >> 1);
+  if (k >= np) return;
+  const uint32_t h = threadIdx.x & 1u;
+  uint32_t use = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; j++) {
+    const uint64_t r = (uint64_t)RPL * k + j;
+    if (r < m && code[r] == 0 && (inf[r] & INF_PK) == 0) use |= 1u << j;
+  }
+  auto out_row = [&](int kk, int q) { return fout + (uint64_t)(6 * kk + 3 * h + q) * fstride + k; };
+  if (!use) {   // one
+#pragma unroll 1
+    for (int kk = 0; kk < 6; kk++) {
+      const fph v = kk ? fph_zero() : fph_one();
+#pragma unroll
+      for (int q = 0; q < 3; q++)
+        *out_row(kk, q) = make_uint4(v.v.v[4 * q], v.v.v[4 * q + 1], v.v.v[4 * q + 2], v.v.v[4 * q + 3]);
+    }
+    return;
+  }
+  __shared__ uint4 G[18][CESS_PAIR_THREADS];
+  LdsPair f{G, wave_first_thread()};
+  const uint32_t r0 = RPL * k;
+  auto pt = [&](int j) {
+    return g1a{ld_fp(h_aff, stride, r0 + j), ld_fp(h_aff + 12 * stride, stride, r0 + j), false};
+  };
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  auto src = [&](int j, int s, fph& k0, fph& k1, fph& k2) {
+    fph* c[3] = {&k0, &k1, &k2};
+#pragma unroll
+    for (int cc = 0; cc < 3; cc++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const u4v x =
+            __builtin_nontemporal_load((const u4v*)(coeffs + (uint64_t)(18 * s + 6 * cc + 3 * h + q) * stride + r0 + j));
+        c[cc]->v.v[4 * q] = x.x, c[cc]->v.v[4 * q + 1] = x.y, c[cc]->v.v[4 * q + 2] = x.z, c[cc]->v.v[4 * q + 3] = x.w;
+      }
+  };
+  miller_loopn_pair<RPL>(f, use, pt, src);
+#pragma unroll 1
+  for (int kk = 0; kk < 6; kk++) {
+    const fph v = f.ld(kk);
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+      *out_row(kk, q) = make_uint4(v.v.v[4 * q], v.v.v[4 * q + 1], v.v.v[4 * q + 2], v.v.v[4 * q + 3]);
   }
 }

@@ -38,6 +38,12 @@ enum : uint8_t { INF_SIG = 1, INF_PK = 2 };
 #define CESS_MSM_SEG_BUCKETS 4096u
 // records per lane of the distinct-key RLC's Miller values (k_miller_rr): a
 // lane's value is the product of its records' Miller values
+// threads per block of the lane-pair kernels (k_miller2, k_final2): two lanes
+// per signature, an 18 x CESS_PAIR_THREADS uint4 LDS image per block, two
+// waves per SIMD whatever the block size
+#ifndef CESS_PAIR_THREADS
+#define CESS_PAIR_THREADS 256
+#endif
 #ifndef CESS_RLCD_PER
 #define CESS_RLCD_PER 4
 #endif

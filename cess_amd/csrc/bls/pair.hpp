@@ -264,6 +264,29 @@ CESS_HD fph pdot2_p(const pxd& x, const pyd& y, const pxd& u, const pyd& w) {
   return {r};
 }
 
+// this lane's component of x y + u w + s t from prepared operands: ONE
+// reduction over six half-products.  Columns < 3 x 14 x (2^56 + 2^57) + 14 x
+// 2^56 < 2^63.2 (x digits < 2^28, y digits < 2^29: K - b1), and the value
+// < 3 x 8p x 2^385 < p R for inputs < 8p, so the reduction returns < 2p.
+CESS_HD fph pdot3_p(const pxd& x, const pyd& y, const pxd& u, const pyd& w, const pxd& s, const pyd& t) {
+  CESS_COUNT_HALVES(12);
+  fp r = mont28([&](int k, int h, uint64_t& acc) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= 14 || (h >= 0 && (i & 1) != h)) continue;
+      mac(acc, x.a[i], y.a[j]);
+      mac(acc, x.b[i], y.b[j]);
+      mac(acc, u.a[i], w.a[j]);
+      mac(acc, u.b[i], w.b[j]);
+      mac(acc, s.a[i], t.a[j]);
+      mac(acc, s.b[i], t.b[j]);
+    }
+  });
+  seq(r);
+  return {r};
+}
+
 // a * s for s in Fp (both lanes hold s): one Fp product per lane
 CESS_HD fph pmul_fp(const fph& a, const fp& s) { return {mul(a.v, s)}; }
 
@@ -276,8 +299,46 @@ CESS_HD fp6h add_nr(const fp6h& a, const fp6h& b) {
 }
 CESS_HD fp6h mul_v(const fp6h& a) { return {mul_nr(a.c2), a.c0, a.c1}; }
 
+// Schoolbook Fp6 product as three lazily reduced dot products (one reduction
+// per output component; v^3 = xi):
+//   c0 = a0 b0 + a1 (xi b2) + a2 (xi b1),  c1 = a0 b1 + a1 b0 + a2 (xi b2),
+//   c2 = a0 b2 + a1 b1 + a2 b0.
+// 17 % more mads than Karatsuba's six products, but the three x operands and
+// five y operands are prepared once (unpack + DPP exchange) and there are no
+// operand sums, no re-preparation of them and no recombination: fewer VALU
+// instructions per Fp6 product (CESS_PAIR_SB).  a(j): this lane's component of
+// a's coefficient j (a loader or register values), < 8p; b's coefficients < 4p.
+// Measured, not adopted: static VALU -2.5 % (k_miller2) / -2.9 % (k_final2),
+// but 15 / 62 spilled VGPRs, and equal time on the same box (k_miller2
+// 126.8-126.9 vs 126.7-127.0, k_final2 140.8-141.9 vs 140.9-141.0 ms,
+// profiles/round6_k_sweep_schoolbook.txt).
+#ifndef CESS_PAIR_SB
+#define CESS_PAIR_SB 0
+#endif
+template <class LA>
+CESS_HD fp6h pmul6_sb(LA&& a, const fp6h& b) {
+  const pxd x0 = prep_x(a(0)), x1 = prep_x(a(1)), x2 = prep_x(a(2));
+  fp6h c;
+  {
+    const pyd y0 = prep_y(b.c0), y1 = prep_y(b.c1);
+    c.c2 = pdot3_p(x0, prep_y(b.c2), x1, y1, x2, y0);
+    CESS_MEMBAR();
+    // xi b2, xi b1 from b reduced below 2p: callers pass unreduced sums (< 4p:
+    // add_nr(a0, v a1) in the squaring, g0 + g1 in FE_MUL), and xi's 2p - b
+    // on the even lane needs b < 2p
+    const pyd xy2 = prep_y(mul_nr_nr(fph{fp_reduce2(b.c2.v)}));
+    c.c1 = pdot3_p(x0, y1, x1, y0, x2, xy2);
+    CESS_MEMBAR();
+    c.c0 = pdot3_p(x0, y0, x1, xy2, x2, prep_y(mul_nr_nr(fph{fp_reduce2(b.c1.v)})));
+  }
+  return c;
+}
+
 // Karatsuba Fp6 product (as field.hpp mul(fp6, fp6))
 CESS_HD fp6h pmul6(const fp6h& a, const fp6h& b) {
+#if CESS_PAIR_SB
+  return pmul6_sb([&](int j) { return j == 0 ? a.c0 : j == 1 ? a.c1 : a.c2; }, b);
+#endif
   const fph t0 = pmul(a.c0, b.c0);
   const fph t1 = pmul(a.c1, b.c1);
   const fph t2 = pmul(a.c2, b.c2);

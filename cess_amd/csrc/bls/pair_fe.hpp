@@ -100,6 +100,9 @@ CESS_HD bool pis_conj12(const A& a, const B& b) {
 // the second held in registers
 template <class LA>
 CESS_HD fp6h pmul6_lr(LA&& a, const fp6h& b) {
+#if CESS_PAIR_SB
+  return pmul6_sb(a, b);
+#endif
   const fph v0 = pmul(a(0), b.c0);
   CESS_MEMBAR();
   const fph v1 = pmul(a(1), b.c1);

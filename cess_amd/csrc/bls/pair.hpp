@@ -498,8 +498,11 @@ CESS_HD void pmul014_one(const S& f, const fph& c1, const fph& c4) {
 }
 
 // The two-pair Miller loop of staged.hpp miller_loop2_staged over a lane
-// pair: pt(pair) the pair's affine G1 point (both lanes), src(pair, step, c1,
-// c2, c4): this lane's components of the line's (c0, c1, c2) coefficients.
+// pair: pt(pair) the pair's affine G1 point (both lanes), src(pair, step, j):
+// this lane's component of the line's coefficient c_j (returned by value:
+// coefficients written through reference parameters from pair-dependent
+// branches were lowered to a dynamically indexed private array -- ~40
+// scratch accesses per Miller step).
 template <class S, class Pt, class Src>
 CESS_HD void miller_loop2_pair(const S& f, bool use0, bool use1, Pt&& pt, Src&& src, bool norm1) {
   f.st(0, fph_one());
@@ -511,12 +514,10 @@ CESS_HD void miller_loop2_pair(const S& f, bool use0, bool use1, Pt&& pt, Src&& 
     for (int pair = 0; pair < 2; pair++) {
       const int pr = 1 - pair;
       if (!(pr ? use1 : use0)) continue;
-      fph k0, k1, k2;
-      src(pr, s, k0, k1, k2);
       const g1a p = pt(pr);
-      const fph c1 = pmul_fp(k1, p.x), c4 = pmul_fp(k0, p.y);
+      const fph c1 = pmul_fp(src(pr, s, 1), p.x), c4 = pmul_fp(src(pr, s, 0), p.y);
       if (pr && !norm1)
-        pmul014(f, k2, c1, c4);
+        pmul014(f, src(pr, s, 2), c1, c4);
       else
         pmul014_one(f, c1, c4);
       CESS_MEMBAR();
@@ -531,8 +532,8 @@ CESS_HD void miller_loop2_pair(const S& f, bool use0, bool use1, Pt&& pt, Src&& 
 // Miller loop over up to NP pairs with general lines sharing one accumulator
 // (staged.hpp miller_loopn_staged, the distinct-key RLC's lane of records) on
 // a lane pair: bit j of `use` (the same in both lanes) -- pair j takes part;
-// pt(j) its affine G1 point, src(j, step, k0, k1, k2) this lane's components
-// of its line coefficients.
+// pt(j) its affine G1 point, src(j, step, c) this lane's component of its
+// line coefficient c (by value, as in miller_loop2_pair).
 template <int NP, class S, class Pt, class Src>
 CESS_HD void miller_loopn_pair(const S& f, uint32_t use, Pt&& pt, Src&& src) {
   f.st(0, fph_one());
@@ -543,10 +544,9 @@ CESS_HD void miller_loopn_pair(const S& f, uint32_t use, Pt&& pt, Src&& src) {
 #pragma unroll 1
     for (int j = 0; j < NP; j++) {
       if (!((use >> j) & 1u)) continue;
-      fph k0, k1, k2;
-      src(j, s, k0, k1, k2);
       const g1a p = pt(j);
-      pmul014(f, k2, pmul_fp(k1, p.x), pmul_fp(k0, p.y));
+      const fph c1 = pmul_fp(src(j, s, 1), p.x), c4 = pmul_fp(src(j, s, 0), p.y);
+      pmul014(f, src(j, s, 2), c1, c4);
       CESS_MEMBAR();
     }
     if (square_after_step(s)) psqr12(f);

@@ -33,17 +33,28 @@ __global__ __launch_bounds__(CESS_PAIR_THREADS, 2) void k_miller2(uint64_t n, co
   const uint8_t fl = inf[i];
   __shared__ uint4 G[18][CESS_PAIR_THREADS];
   LdsPair f{G, wave_first_thread()};
-  auto pt = [&](int pair) {
+  // (the lambdas capture by value: with [&] captures the compiler kept the
+  // captured pointers in a private frame and selected the pair's point through
+  // it -- a dozen scratch accesses per line at 256 registers. The per-lane
+  // offsets pass through an empty asm so each address is re-formed at its load
+  // -- one 64-bit add -- instead of a dozen strength-reduced 64-bit pointers
+  // held live, and spilled, across the step.)
+  auto pt = [=](int pair) {
     const uint32_t* b = pair ? h_aff : sig_aff;
-    return g1a{ld_fp(b, stride, i), ld_fp(b + 12 * stride, stride, i), false};
+    uint32_t io = i;
+    asm volatile("" : "+v"(io));
+    return g1a{ld_fp(b, stride, io), ld_fp(b + 12 * stride, stride, io), false};
   };
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const uint64_t vo_c = 3 * h * cstride + cj, vo_t = 3 * h;
   // this lane's component of line coefficient j: rows 18k + 6j + 3h .. + 2
-  auto ld_row = [&](const uint4* base, uint64_t st, uint32_t col, int k, int j, bool nt) {
+  // (vo = 3h st + column, this lane's offset)
+  auto ld_row = [=](const uint4* base, uint64_t st, uint64_t vo, int k, int j, bool nt) {
     fph r;
+    asm volatile("" : "+v"(vo));
 #pragma unroll
     for (int q = 0; q < 3; q++) {
-      const uint4* a = base + (uint64_t)(18 * k + 6 * j + 3 * h + q) * st + col;
+      const uint4* a = base + (uint64_t)(18 * k + 6 * j + q) * st + vo;
       u4v x;
       if (nt)
         x = __builtin_nontemporal_load((const u4v*)a);
@@ -54,17 +65,9 @@ __global__ __launch_bounds__(CESS_PAIR_THREADS, 2) void k_miller2(uint64_t n, co
     return r;
   };
   const uint4* g2tab = (const uint4*)neg_g2;   // 72 dwords = 18 uint4 per line, stride 1
-  auto src = [&](int pair, int k, fph& k0, fph& k1, fph& k2) {
-    if (pair) {
-      const bool nt = cidx == nullptr;
-      k0 = ld_row(coeffs, cstride, cj, k, 0, nt);
-      k1 = ld_row(coeffs, cstride, cj, k, 1, nt);
-      k2 = ld_row(coeffs, cstride, cj, k, 2, nt);
-    } else {
-      // -G2 table normalised to c2 = 1: c0 and c1 only
-      k0 = ld_row(g2tab, 1, 0, k, 0, false);
-      k1 = ld_row(g2tab, 1, 0, k, 1, false);
-    }
+  // (the -G2 table is normalised to c2 = 1: pair 0 reads c0 and c1 only)
+  auto src = [=](int pair, int k, int j) {
+    return pair ? ld_row(coeffs, cstride, vo_c, k, j, cidx == nullptr) : ld_row(g2tab, 1, vo_t, k, j, false);
   };
   const bool norm1 = cnorm && cnorm[cj];
   miller_loop2_pair(f, (fl & INF_SIG) == 0, (fl & INF_PK) == 0, pt, src, norm1);
@@ -116,20 +119,24 @@ __global__ __launch_bounds__(CESS_PAIR_THREADS, 2) void k_miller_rr2(uint64_t np
   __shared__ uint4 G[18][CESS_PAIR_THREADS];
   LdsPair f{G, wave_first_thread()};
   const uint32_t r0 = RPL * k;
-  auto pt = [&](int j) {
-    return g1a{ld_fp(h_aff, stride, r0 + j), ld_fp(h_aff + 12 * stride, stride, r0 + j), false};
+  // (offsets through an empty asm, as in k_miller2: addresses re-formed at
+  // each load rather than strength-reduced pointers spilled across the lane)
+  auto pt = [=](int j) {
+    uint32_t io = r0 + j;
+    asm volatile("" : "+v"(io));
+    return g1a{ld_fp(h_aff, stride, io), ld_fp(h_aff + 12 * stride, stride, io), false};
   };
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  auto src = [&](int j, int s, fph& k0, fph& k1, fph& k2) {
-    fph* c[3] = {&k0, &k1, &k2};
+  auto src = [=](int j, int s, int cc) {
+    fph c;
+    uint64_t vo = 3 * h * stride + r0 + j;
+    asm volatile("" : "+v"(vo));
 #pragma unroll
-    for (int cc = 0; cc < 3; cc++)
-#pragma unroll
-      for (int q = 0; q < 3; q++) {
-        const u4v x =
-            __builtin_nontemporal_load((const u4v*)(coeffs + (uint64_t)(18 * s + 6 * cc + 3 * h + q) * stride + r0 + j));
-        c[cc]->v.v[4 * q] = x.x, c[cc]->v.v[4 * q + 1] = x.y, c[cc]->v.v[4 * q + 2] = x.z, c[cc]->v.v[4 * q + 3] = x.w;
-      }
+    for (int q = 0; q < 3; q++) {
+      const u4v x = __builtin_nontemporal_load((const u4v*)(coeffs + (uint64_t)(18 * s + 6 * cc + q) * stride + vo));
+      c.v.v[4 * q] = x.x, c.v.v[4 * q + 1] = x.y, c.v.v[4 * q + 2] = x.z, c.v.v[4 * q + 3] = x.w;
+    }
+    return c;
   };
   miller_loopn_pair<RPL>(f, use, pt, src);
 #pragma unroll 1

@@ -149,15 +149,52 @@ CESS_HD fp fp_reduce2(const fp& t) {
   return r;
 }
 
+// a + b < 4p < 2^383 (no carry out of limb 11), then - 2p if >= 2p.  The sum
+// and the trial subtraction run as two chains interleaved limb by limb (the
+// subtraction's limb i needs only the sum's limb i): one chain alone waits two
+// states on its carry register between links (s_nop 1 per link on gfx950),
+// two interleaved chains one.
+#ifndef CESS_ADD_ILV
+#define CESS_ADD_ILV 1
+#endif
 CESS_HD fp add(const fp& a, const fp& b) {
+#if CESS_ADD_ILV
+  fp t, s;
+  uint32_t carry = 0, borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    t.v[i] = addc32(a.v[i], b.v[i], carry, &carry);
+    s.v[i] = subc32(t.v[i], c::P2_RAW[i], borrow, &borrow);
+  }
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = borrow ? t.v[i] : s.v[i];
+  return r;
+#else
   fp t;
   uint32_t carry = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) t.v[i] = addc32(a.v[i], b.v[i], carry, &carry);
-  return fp_reduce2(t);  // a + b < 4p < 2^383: no carry out of limb 11
+  return fp_reduce2(t);
+#endif
 }
 
 CESS_HD fp sub(const fp& a, const fp& b) {
+#if CESS_ADD_ILV
+  // a - b and a - b + 2p as two interleaved chains (as add), the second kept
+  // if the first borrows (a - b > -2p)
+  fp t, u;
+  uint32_t borrow = 0, carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    t.v[i] = subc32(a.v[i], b.v[i], borrow, &borrow);
+    u.v[i] = addc32(t.v[i], c::P2_RAW[i], carry, &carry);
+  }
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = borrow ? u.v[i] : t.v[i];
+  return r;
+#else
   fp t;
   uint32_t borrow = 0;
 #pragma unroll
@@ -169,6 +206,7 @@ CESS_HD fp sub(const fp& a, const fp& b) {
 #pragma unroll
   for (int i = 0; i < 12; i++) r.v[i] = addc32(t.v[i], c::P2_RAW[i] & mask, carry, &carry);
   return r;
+#endif
 }
 
 // Unreduced sum (no conditional subtraction): a + b < 4p for a, b < 2p.

@@ -870,6 +870,16 @@ CESS_HD fp2 fp2_one() { return {fp_one(), fp_zero()}; }
 CESS_HD fp2 add(const fp2& a, const fp2& b) {
   fp t0, t1, s0, s1;
   uint32_t c0 = 0, c1 = 0, b0 = 0, b1 = 0;
+#if CESS_ADD_ILV
+  // the two sums and their trial subtractions: four chains, no wait states
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    t0.v[i] = addc32(a.c0.v[i], b.c0.v[i], c0, &c0);
+    t1.v[i] = addc32(a.c1.v[i], b.c1.v[i], c1, &c1);
+    s0.v[i] = subc32(t0.v[i], c::P2_RAW[i], b0, &b0);
+    s1.v[i] = subc32(t1.v[i], c::P2_RAW[i], b1, &b1);
+  }
+#else
 #pragma unroll
   for (int i = 0; i < 12; i++) {
     t0.v[i] = addc32(a.c0.v[i], b.c0.v[i], c0, &c0);
@@ -880,6 +890,7 @@ CESS_HD fp2 add(const fp2& a, const fp2& b) {
     s0.v[i] = subc32(t0.v[i], c::P2_RAW[i], b0, &b0);
     s1.v[i] = subc32(t1.v[i], c::P2_RAW[i], b1, &b1);
   }
+#endif
   fp2 r;
 #pragma unroll
   for (int i = 0; i < 12; i++) {
@@ -889,6 +900,25 @@ CESS_HD fp2 add(const fp2& a, const fp2& b) {
   return r;
 }
 CESS_HD fp2 sub(const fp2& a, const fp2& b) {
+#if CESS_ADD_ILV
+  // the two differences and the same plus 2p: four chains, no wait states
+  fp t0, t1, u0, u1;
+  uint32_t b0 = 0, b1 = 0, c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    t0.v[i] = subc32(a.c0.v[i], b.c0.v[i], b0, &b0);
+    t1.v[i] = subc32(a.c1.v[i], b.c1.v[i], b1, &b1);
+    u0.v[i] = addc32(t0.v[i], c::P2_RAW[i], c0, &c0);
+    u1.v[i] = addc32(t1.v[i], c::P2_RAW[i], c1, &c1);
+  }
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.v[i] = b0 ? u0.v[i] : t0.v[i];
+    r.c1.v[i] = b1 ? u1.v[i] : t1.v[i];
+  }
+  return r;
+#else
   fp t0, t1;
   uint32_t b0 = 0, b1 = 0, c0 = 0, c1 = 0;
 #pragma unroll
@@ -904,6 +934,7 @@ CESS_HD fp2 sub(const fp2& a, const fp2& b) {
     r.c1.v[i] = addc32(t1.v[i], c::P2_RAW[i] & m1, c1, &c1);
   }
   return r;
+#endif
 }
 // unreduced, for mul() operands only (see add_nr(fp, fp))
 CESS_HD fp2 add_nr(const fp2& a, const fp2& b) {

@@ -277,53 +277,57 @@ CESS_HD void pkcyc_run(fph& z2, fph& z3, fph& z4, fph& z5, int n) {
   }
 }
 
-// 2p - a (in (0, 2p] for a in [0, 2p)): a negation for add() only
-CESS_HD fp2 neg_2p(const fp2& a) {
-  fp2 r;
-  uint32_t b0 = 0, b1 = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    r.c0.v[i] = subc32(c::P2_RAW[i], a.c0.v[i], b0, &b0);
-    r.c1.v[i] = subc32(c::P2_RAW[i], a.c1.v[i], b1, &b1);
-  }
-  return r;
-}
 CESS_HD fp2 xchg2(const fp2& a) { return {xchg(a.c0), xchg(a.c1)}; }
 
 // n Karabina compressed squarings split by PRODUCTS over the pair: the
 // squaring's two halves are independent -- (z4, z5) gives 3 (z4^2 + xi z5^2)
 // and 6 xi z4 z5, which update z3 and z2; (z2, z3) gives 3 (z2^2 + xi z3^2)
-// and 6 z2 z3, which update z4 and z5 -- so lane 0 holds (u, w) = (z4, z5)
-// and lane 1 (u, w) = (z2, z3) as FULL Fp2 values, each runs its half's two
-// lazily reduced products (mul_scaled<3>, no per-product exchange) and the
-// lanes swap two Fp2 results per squaring.  Per signature ~8 % fewer VALU
-// instructions than the component-split pkcyc_run.  With A = 3 (u^2 + xi w^2),
-// b3 = 3 u w: lane 0 sends (2 xi b3, A), lane 1 sends (A, 2 b3), and with
-// (f, s) received
-//   lane 0:  z4' = f - 2 z4,  z5' = s + 2 z5
-//   lane 1:  z2' = f + 2 z2,  z3' = s - 2 z3.
+// and 6 z2 z3, which update z4 and z5 -- so each lane holds one half as FULL
+// Fp2 values, runs its two lazily reduced products (mul_scaled<3>, no
+// per-product exchange) and the lanes swap two Fp2 results per squaring.
+// Lane 0 holds (u, w) = (z4, z5), lane 1 (u, w) = (z3, z2), so that both
+// lanes apply the same update to what they receive:
+//   b3 = 3 u w,  A = 3 (u^2 + xi w^2) on lane 0, 3 (w^2 + xi u^2) on lane 1
+//   (the second product's operand is u + xi w or w + xi u);
+//   lane 0 sends (A, xi b3), lane 1 sends (A, b3); with (P, Q) received
+//   u' = P - 2u,  w' = 2 (w + Q)
+// (lane 0: z4' = 3 (z2^2 + xi z3^2) - 2 z4, z5' = 2 (z5 + 3 z2 z3); lane 1:
+// z3' = 3 (z4^2 + xi z5^2) - 2 z3, z2' = 2 (z2 + 3 xi z4 z5)).
+// (u + w, u + xi w | w + xi u), unreduced (< 4p, < 6p), in one pass: the
+// xi term is the lane's own select of (w, u)
+CESS_HD void ps_operands(const fp2& u, const fp2& w, bool hi, fp2& s, fp2& y) {
+  uint32_t bn = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t z0 = hi ? u.c0.v[i] : w.c0.v[i], z1 = hi ? u.c1.v[i] : w.c1.v[i];
+    const uint32_t nz1 = subc32(c::P2_RAW[i], z1, bn, &bn);
+    s.c0.v[i] = addc32(u.c0.v[i], w.c0.v[i], k0, &k0);
+    s.c1.v[i] = addc32(u.c1.v[i], w.c1.v[i], k1, &k1);
+    y.c0.v[i] = addc32(s.c0.v[i], nz1, k2, &k2);   // x0 + z0 - z1, {x, z} = {u, w}
+    y.c1.v[i] = addc32(s.c1.v[i], z0, k3, &k3);    // x1 + z1 + z0
+  }
+}
 CESS_HD void pkcyc_run_ps(fp2& u, fp2& w, int n) {
   const bool hi = pair_hi_mask() != 0;
 #pragma unroll 1
   for (int r = 0; r < n; r++) {
     CESS_MEMBAR();
-    fp2 f, sc;
+    fp2 P, Q;
     {
       const fp2 b3 = mul_scaled<3>(u, w);
       CESS_MEMBAR();
-      const fp2 t3 = mul_scaled<3>(add_nr(u, w), add_xi_nr(u, w));
+      fp2 s, y;
+      ps_operands(u, w, hi, s, y);
+      const fp2 t3 = mul_scaled<3>(s, y);
       const fp2 nb3 = mul_nr(b3);
-      const fp2 A = sub(sub(t3, b3), nb3);
-      const fp2 D = dbl(select(hi, b3, nb3));
-      f = select(hi, A, D);
-      sc = select(hi, D, A);
+      P = sub(sub(t3, b3), nb3);
+      Q = select(hi, b3, nb3);
     }
     CESS_MEMBAR();
-    f = xchg2(f);
-    sc = xchg2(sc);
-    const fp2 du = dbl(u), dw = dbl(w);
-    u = add(f, select(hi, du, neg_2p(du)));
-    w = add(sc, select(hi, neg_2p(dw), dw));
+    P = xchg2(P);
+    Q = xchg2(Q);
+    u = sub(P, dbl(u));
+    w = dbl(add(w, Q));
   }
 }
 
@@ -351,9 +355,9 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
 #endif
 #if CESS_PAIR_KCYC_PS
   {
-    // store indices of (u, w): lane 0 (z4, z5) = (1, 5), lane 1 (z2, z3) = (3, 2)
+    // store indices of (u, w): lane 0 (z4, z5) = (1, 5), lane 1 (z3, z2) = (2, 3)
     const bool hi = pair_hi_mask() != 0;
-    const int ku = hi ? 3 : 1, kw = hi ? 2 : 5;
+    const int ku = hi ? 2 : 1, kw = hi ? 3 : 5;
     fp2 u = base.ld_full(ku), w = base.ld_full(kw);
     int k = 0;
 #pragma unroll 1

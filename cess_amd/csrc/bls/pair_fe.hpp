@@ -210,22 +210,19 @@ CESS_HD void pfrob12(const S& f, int k) {
 }
 
 // (a + b s)^2 in Fp4 (field.hpp fp4_square)
+// (a + b s)^2 = (a^2 + xi b^2) + 2 a b s in two products, as the Karabina
+// squaring: t0 = a b, t = (a + b)(a + xi b) = a^2 + xi b^2 + (1 + xi) a b
+// (against three: a^2, b^2, (a + b)^2)
 CESS_HD void pfp4_square(fph& c0, fph& c1, const fph& a, const fph& b) {
-  const fph t0 = pmul(a, a);
+  const fph t0 = pmul(a, b);
   CESS_MEMBAR();
-  const fph t1 = pmul(b, b);
-  CESS_MEMBAR();
-  c0 = add(mul_nr(t1), t0);
-  const fph s = add_nr(a, b);
-  c1 = sub(sub(pmul(s, s), t0), t1);
+  const fph t = pmul(add_nr(a, b), add_xi_nr(a, b));
+  c0 = sub(sub(t, t0), mul_nr(t0));
+  c1 = dbl(t0);
 }
-// n Granger-Scott cyclotomic squarings of the store f (staged.hpp
-// cyc_square_run / cycsq12), the six coefficients in registers (72 per lane)
-template <class S>
-CESS_HD void pcyc_square_run(const S& f, int n) {
-  fph z[6];
-#pragma unroll
-  for (int k = 0; k < 6; k++) z[k] = f.ld(k);
+// n Granger-Scott cyclotomic squarings (staged.hpp cyc_square_run / cycsq12)
+// of the six coefficients z (in registers, 72 per lane)
+CESS_HD void pcyc_square_regs(fph (&z)[6], int n) {
 #pragma unroll 1
   for (int r = 0; r < n; r++) {
     CESS_MEMBAR();
@@ -244,6 +241,14 @@ CESS_HD void pcyc_square_run(const S& f, int n) {
     z[3] = add(dbl(add(n3, z[3])), n3);
     z[2] = add(dbl(sub(t2, z[2])), t2);
   }
+}
+// n Granger-Scott squarings of the store f in place
+template <class S>
+CESS_HD void pcyc_square_run(const S& f, int n) {
+  fph z[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) z[k] = f.ld(k);
+  pcyc_square_regs(z, n);
 #pragma unroll
   for (int k = 0; k < 6; k++) f.st(k, z[k]);
 }
@@ -347,9 +352,18 @@ CESS_HD fph pcyc_z0(const fph& z1, const fph& z2, const fph& z3, const fph& z4, 
 }
 
 // FE_CHAIN (staged.hpp cyc_chain): the powers a^(2^k), k = 16, 48, 57, 60, 62,
-// 63, of the cyclotomic element in `base` into the stores X(0..5)
+// 63, of the cyclotomic element in `base` into the stores X(0..5).
+// CESS_PAIR_CHAIN_TAIL (default 1): only a^(2^16), a^(2^48) and a^(2^57) come
+// from the compressed run and its decompression; a^(2^60), a^(2^62) and
+// a^(2^63) follow from a^(2^57) by 3 + 2 + 1 Granger-Scott squarings.  Per
+// exponentiation by x that is 6 GS squarings (6 products each, against 4 for
+// a Karabina squaring) for 3 decompressions (~8.5 products each).
+#ifndef CESS_PAIR_CHAIN_TAIL
+#define CESS_PAIR_CHAIN_TAIL 1
+#endif
 template <class B, class XFn>
 CESS_HD void pcyc_chain(const B& base, XFn&& X) {
+  constexpr int ND = CESS_PAIR_CHAIN_TAIL ? 3 : 6;   // decompressed powers
 #ifndef CESS_PAIR_KCYC_PS
 #define CESS_PAIR_KCYC_PS 1
 #endif
@@ -361,7 +375,7 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
     fp2 u = base.ld_full(ku), w = base.ld_full(kw);
     int k = 0;
 #pragma unroll 1
-    for (int j = 0; j < 6; j++) {
+    for (int j = 0; j < ND; j++) {
       const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
       pkcyc_run_ps(u, w, stop - k);
       k = stop;
@@ -376,7 +390,7 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
     fph z4 = base.ld(1), z5 = base.ld(5), z2 = base.ld(3), z3 = base.ld(2);
     int k = 0;
 #pragma unroll 1
-    for (int j = 0; j < 6; j++) {
+    for (int j = 0; j < ND; j++) {
       const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
       pkcyc_run(z2, z3, z4, z5, stop - k);
       k = stop;
@@ -393,7 +407,7 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
   bool degen = false;
   fph prod = fph_one();
 #pragma unroll 1
-  for (int j = 0; j < 6; j++) {
+  for (int j = 0; j < ND; j++) {
     const auto x = X(j);
     fph num, den;
     pcyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
@@ -406,7 +420,7 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
   }
   fph iv = pinv(prod);
 #pragma unroll 1
-  for (int j = 5; j >= 0; j--) {
+  for (int j = ND - 1; j >= 0; j--) {
     const auto x = X(j);
     const fph den = pcyc_z1_den(x.ld(3), x.ld(2));
     const fph ivj = pmul(iv, x.ld(0));   // 1 / den_j
@@ -429,6 +443,24 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
     }
     pcyc_square_run(w, 1);
   }
+#if CESS_PAIR_CHAIN_TAIL
+  else {   // X3..X5 from X2 = a^(2^57): 3, 2, 1 squarings
+    fph z[6];
+    {
+      const auto x2 = X(2);
+#pragma unroll
+      for (int k = 0; k < 6; k++) z[k] = x2.ld(k);
+    }
+#pragma unroll 1
+    for (int j = 3; j < 6; j++) {
+      pcyc_square_regs(z, j == 3 ? 3 : j == 4 ? 2 : 1);
+      CESS_MEMBAR();
+      const auto x = X(j);
+#pragma unroll
+      for (int k = 0; k < 6; k++) x.st(k, z[k]);
+    }
+  }
+#endif
 }
 
 // The program (staged.hpp final_exp_staged) on ONE in-place accumulator

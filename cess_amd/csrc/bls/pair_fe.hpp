@@ -353,17 +353,14 @@ CESS_HD fph pcyc_z0(const fph& z1, const fph& z2, const fph& z3, const fph& z4, 
 
 // FE_CHAIN (staged.hpp cyc_chain): the powers a^(2^k), k = 16, 48, 57, 60, 62,
 // 63, of the cyclotomic element in `base` into the stores X(0..5).
-// CESS_PAIR_CHAIN_TAIL (default 1): only a^(2^16), a^(2^48) and a^(2^57) come
-// from the compressed run and its decompression; a^(2^60), a^(2^62) and
-// a^(2^63) follow from a^(2^57) by 3 + 2 + 1 Granger-Scott squarings.  Per
-// exponentiation by x that is 6 GS squarings (6 products each, against 4 for
-// a Karabina squaring) for 3 decompressions (~8.5 products each).
-#ifndef CESS_PAIR_CHAIN_TAIL
-#define CESS_PAIR_CHAIN_TAIL 1
-#endif
+// CESS_CHAIN_TAIL (staged.hpp, default 1): only a^(2^16), a^(2^48) and
+// a^(2^57) come from the compressed run and its decompression; a^(2^60),
+// a^(2^62) and a^(2^63) follow from a^(2^57) by 3 + 2 + 1 Granger-Scott
+// squarings.  Per exponentiation by x that is 6 GS squarings (6 products each,
+// against 4 for a Karabina squaring) for 3 decompressions (~8.5 products each).
 template <class B, class XFn>
 CESS_HD void pcyc_chain(const B& base, XFn&& X) {
-  constexpr int ND = CESS_PAIR_CHAIN_TAIL ? 3 : 6;   // decompressed powers
+  constexpr int ND = CESS_CHAIN_TAIL ? 3 : 6;   // decompressed powers
 #ifndef CESS_PAIR_KCYC_PS
 #define CESS_PAIR_KCYC_PS 1
 #endif
@@ -443,7 +440,7 @@ CESS_HD void pcyc_chain(const B& base, XFn&& X) {
     }
     pcyc_square_run(w, 1);
   }
-#if CESS_PAIR_CHAIN_TAIL
+#if CESS_CHAIN_TAIL
   else {   // X3..X5 from X2 = a^(2^57): 3, 2, 1 squarings
     fph z[6];
     {

@@ -745,21 +745,29 @@ CESS_HD fp2 cyc_z0(const fp2& z1, const fp2& z2, const fp2& z3, const fp2& z4, c
 }
 
 // FE_CHAIN: the powers a^(2^k), k = 16, 48, 57, 60, 62, 63, of the cyclotomic
-// element a (store `base`) into the stores X(0..5): 63 compressed squarings,
-// then z1 of all six powers with ONE Fp2 inversion (Montgomery's simultaneous
-// inversion: numerators parked in the z1 words, prefix products of the
-// denominators in the z0 words; safegcd inversion), then z0.  A lane whose
-// denominator vanishes (z2 = z3 = 0, e.g. a = 1 from an identity pair) redoes
-// its chain with Granger-Scott squarings (divergent, rare).
+// element a (store `base`) into the stores X(0..5): compressed squarings, then
+// z1 of the compressed powers with ONE Fp2 inversion (Montgomery's
+// simultaneous inversion: numerators parked in the z1 words, prefix products
+// of the denominators in the z0 words; safegcd inversion), then z0.  A lane
+// whose denominator vanishes (z2 = z3 = 0, e.g. a = 1 from an identity pair)
+// redoes its chain with Granger-Scott squarings (divergent, rare).
+// CESS_CHAIN_TAIL (default 1): the compressed run stops at a^(2^57); only
+// a^(2^16), a^(2^48), a^(2^57) are decompressed, and a^(2^60), a^(2^62),
+// a^(2^63) follow by 3 + 2 + 1 Granger-Scott squarings -- six uncompressed
+// squarings for three decompressions (pair_fe.hpp pcyc_chain).
+#ifndef CESS_CHAIN_TAIL
+#define CESS_CHAIN_TAIL 1
+#endif
 template <class B, class XFn, class P, class DG = NoDiag>
 CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk, DG* dg = nullptr) {
+  constexpr int ND = CESS_CHAIN_TAIL ? 3 : 6;   // decompressed powers
   {
     pk.st(0, base.ld(1));   // z4, z5 of the running power
     pk.st(1, base.ld(5));
     fp2 z2 = base.ld(3), z3 = base.ld(2);
     int k = 0;
 #pragma unroll 1
-    for (int j = 0; j < 6; j++) {
+    for (int j = 0; j < ND; j++) {
       const int stop = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
       if (dg) dg->template mark<0>();
       kcyc_run(pk, z2, z3, stop - k);
@@ -777,7 +785,7 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk, DG* dg = nullptr) {
   bool degen = false;
   fp2 prod = fp2_one();
 #pragma unroll 1
-  for (int j = 0; j < 6; j++) {
+  for (int j = 0; j < ND; j++) {
     const auto x = X(j);
     fp2 num, den;
     cyc_z1_frac(x.ld(3), x.ld(2), x.ld(1), x.ld(5), num, den);
@@ -790,7 +798,7 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk, DG* dg = nullptr) {
   }
   fp2 iv = inv(prod);
 #pragma unroll 1
-  for (int j = 5; j >= 0; j--) {
+  for (int j = ND - 1; j >= 0; j--) {
     const auto x = X(j);
     const fp2 den = cyc_z1_den(x.ld(3), x.ld(2));
     const fp2 ivj = mul(iv, x.ld(0));   // 1 / den_j
@@ -813,6 +821,15 @@ CESS_HD void cyc_chain(const B& base, XFn&& X, const P& pk, DG* dg = nullptr) {
     }
     cyc_square_run(w, pk, 1);
   }
+#if CESS_CHAIN_TAIL
+  else {   // X3..X5 from X2 = a^(2^57): 3, 2, 1 squarings
+#pragma unroll 1
+    for (int j = 3; j < 6; j++) {
+      copy12(X(j), X(j - 1));
+      cyc_square_run(X(j), pk, j == 3 ? 3 : j == 4 ? 2 : 1);
+    }
+  }
+#endif
   if (dg) dg->template mark<4>();   // decompression (and the rare fallback)
 }
 

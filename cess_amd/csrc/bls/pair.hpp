@@ -164,6 +164,24 @@ CESS_HD fph pmul_scaled(const fph& a0, const fph& b0) {
 }
 CESS_HD fph pmul(const fph& a, const fph& b) { return pmul_scaled<1>(a, b); }
 
+// a^2: ONE Fp product per lane -- component 0 = (a0 + a1)(a0 - a1) on the
+// even lane, component 1 = (2 a1) a0 on the odd lane (against two
+// half-products and the operand exchange of pmul(a, a)); factors < 4p
+CESS_HD fph psqr(const fph& a) {
+  const fp p = xchg(a.v);
+  const bool hi = pair_hi_mask() != 0;
+  fp x, y;
+  uint32_t cx = 0, bn = 0, cy = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    x.v[i] = addc32(a.v.v[i], hi ? a.v.v[i] : p.v[i], cx, &cx);   // a0 + a1 | 2 a1
+    const uint32_t n = subc32(c::P2_RAW[i], p.v[i], bn, &bn);      // 2p - a1
+    const uint32_t t = addc32(a.v.v[i], n, cy, &cy);                // a0 + 2p - a1
+    y.v[i] = hi ? p.v[i] : t;                                       // a0 - a1 | a0
+  }
+  return {mul(x, y)};
+}
+
 // a^-1 in Fp2: a / (a0^2 + a1^2) conjugated (field.hpp inv(fp2)); the norm
 // and its Fp inversion are computed by both lanes
 CESS_HD fph pinv(const fph& a) {

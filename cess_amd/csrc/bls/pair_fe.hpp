@@ -342,13 +342,13 @@ CESS_HD void pcyc_z1_frac(const fph& z2, const fph& z3, const fph& z4, const fph
     num = dbl(pmul(z4, z5));
     den = z3;
   } else {
-    num = sub(add(mul_nr(pmul(z5, z5)), mul3(pmul(z4, z4))), dbl(z3));
+    num = sub(add(mul_nr(psqr(z5)), mul3(psqr(z4))), dbl(z3));
     den = dbl(dbl(z2));
   }
 }
 CESS_HD fph pcyc_z1_den(const fph& z2, const fph& z3) { return is_zero(z2) ? z3 : dbl(dbl(z2)); }
 CESS_HD fph pcyc_z0(const fph& z1, const fph& z2, const fph& z3, const fph& z4, const fph& z5) {
-  return add(mul_nr(add(dbl(pmul(z1, z1)), pdot2(z2, z5, neg(mul3(z3)), z4))), fph_one());
+  return add(mul_nr(add(dbl(psqr(z1)), pdot2(z2, z5, neg(mul3(z3)), z4))), fph_one());
 }
 
 // FE_CHAIN (staged.hpp cyc_chain): the powers a^(2^k), k = 16, 48, 57, 60, 62,

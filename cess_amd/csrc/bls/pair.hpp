@@ -422,8 +422,38 @@ CESS_HD void pst6(const S& s, int h, const fp6h& a) {
 }
 
 // f <- f^2 (complex squaring: 2 Fp6 products), staged.hpp sqr12
+// CESS_PAIR_LOOP (bit mask): the Miller step's repeated Fp6 products as
+// two-iteration loops over ONE inlined product body each -- bit 1 psqr12's two
+// pmul6, bit 2 pmul014's two mul_by_01 halves, bit 4 pmul014_one's -- a
+// smaller step body for the instruction cache (staged.hpp CESS_MUL014_LOOP
+// for k_miller_rr).  Default 5: k_miller2 31.6 K -> 23.7 K instructions,
+// 120.0-120.4 -> 119.5 ms same box (profiles/round6_ab_sweep_loop.txt); bit
+// 2 spills 27 VGPRs (the loop-carried u beside the dot products' operands).
+#ifndef CESS_PAIR_LOOP
+#define CESS_PAIR_LOOP 5
+#endif
 template <class S>
 CESS_HD void psqr12(const S& f) {
+#if CESS_PAIR_LOOP & 1
+  fp6h ab;
+#pragma unroll 1
+  for (int it = 0; it < 2; it++) {
+    const fp6h a0 = pld6(f, 0), a1 = pld6(f, 1);
+    fp6h A = a0, B = a1;
+    if (it) {
+      A = add_nr(a0, a1);
+      B = add_nr(a0, mul_v(a1));
+    }
+    const fp6h r = pmul6(A, B);
+    CESS_MEMBAR();
+    if (it == 0) {
+      ab = r;
+    } else {
+      pst6(f, 0, sub(sub(r, ab), mul_v(ab)));
+      pst6(f, 1, dbl(ab));
+    }
+  }
+#else
   fp6h ab;
   {
     const fp6h a0 = pld6(f, 0), a1 = pld6(f, 1);
@@ -437,6 +467,7 @@ CESS_HD void psqr12(const S& f) {
   }
   pst6(f, 0, sub(sub(x, ab), mul_v(ab)));
   pst6(f, 1, dbl(ab));
+#endif
 }
 
 // a * (b0 + b1 v) for the Fp6 in store half h, as staged.hpp mul_by_01_dot
@@ -471,6 +502,26 @@ template <class S>
 CESS_HD void pmul014(const S& f, const fph& c0, const fph& c1, const fph& c4) {
   const fp6h bb = pmul_by_1(pld6(f, 1), c4);
   CESS_MEMBAR();
+#if CESS_PAIR_LOOP & 2
+  {
+    fp6h u;
+    const fph d = add(c1, c4);
+#pragma unroll 1
+    for (int it = 0; it < 2; it++) {
+      const fph b1 = it ? d : c1;
+      const fp6h r = pmul_by_01_dot(f, it, c0, b1, mul_nr_nr(b1));
+      CESS_MEMBAR();
+      if (it == 0) {
+        pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));   // f.c1 <- a0 + a1 (read by it = 1)
+        pst6(f, 0, add(mul_v(bb), r));
+        u = add(r, bb);
+      } else {
+        pst6(f, 1, sub(r, u));
+      }
+    }
+    return;
+  }
+#endif
   const fp6h aa = pmul_by_01_dot(f, 0, c0, c1, mul_nr_nr(c1));
   CESS_MEMBAR();
   pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));   // f.c1 <- a0 + a1 (consumed below)
@@ -505,6 +556,25 @@ template <class S>
 CESS_HD void pmul014_one(const S& f, const fph& c1, const fph& c4) {
   const fp6h bb = pmul_by_1(pld6(f, 1), c4);
   CESS_MEMBAR();
+#if CESS_PAIR_LOOP & 4
+  {
+    fp6h u;
+    const fph d = add(c1, c4);
+#pragma unroll 1
+    for (int it = 0; it < 2; it++) {
+      const fp6h r = pmul_by_01_one(pld6(f, it), it ? d : c1);
+      CESS_MEMBAR();
+      if (it == 0) {
+        pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));
+        pst6(f, 0, add(mul_v(bb), r));
+        u = add(r, bb);
+      } else {
+        pst6(f, 1, sub(r, u));
+      }
+    }
+    return;
+  }
+#endif
   const fp6h aa = pmul_by_01_one(pld6(f, 0), c1);
   CESS_MEMBAR();
   pst6(f, 1, add(pld6(f, 0), pld6(f, 1)));

@@ -121,8 +121,44 @@ CESS_HD fp6h pmul6_lr(LA&& a, const fp6h& b) {
 // ordered so that at most one Fp6 product is held: t0 = f0 g0;
 // x = (f0 + f1)(g0 + g1); f0 <- x - t0 (f0 is dead: t1 needs f1 only);
 // t1 = f1 g1; f1 <- f0 - t1 = f0 g1 + f1 g0; f0 <- t0 + v t1.
+// CESS_PAIR_FE_LOOP (default 1): the three Fp6 products as a three-iteration
+// loop over ONE inlined pmul6_lr body (a third of the code, as pair.hpp
+// CESS_PAIR_LOOP): k_final2 98.3 K -> 87.3 K instructions, 129.6-129.9 ->
+// 129.1 ms same box (profiles/round6_ac_sweep_feloop.txt)
+#ifndef CESS_PAIR_FE_LOOP
+#define CESS_PAIR_FE_LOOP 1
+#endif
 template <class S, class G>
 CESS_HD void pmul12(const S& f, const G& g) {
+#if CESS_PAIR_FE_LOOP
+  fp6h t0;
+#pragma unroll 1
+  for (int it = 0; it < 3; it++) {
+    // it 0: t0 = f0 g0; it 1: x = (f0 + f1)(g0 + g1); it 2: t1 = f1 g1
+    fp6h b;
+    if (it == 1) {
+      b = add_nr(pld6(g, 0), pld6(g, 1));
+    } else {
+      b = pld6(g, it >> 1);
+    }
+    const fp6h r = pmul6_lr(
+        [&](int j) {
+          const int lo = it == 2 ? 3 : 0;
+          const fph a = f.ld(lo + j);
+          return it == 1 ? add_nr(a, f.ld(3 + j)) : a;
+        },
+        b);
+    CESS_MEMBAR();
+    if (it == 0) {
+      t0 = r;
+    } else if (it == 1) {
+      pst6(f, 0, sub(r, t0));
+    } else {
+      pst6(f, 1, sub(pld6(f, 0), r));
+      pst6(f, 0, add(t0, mul_v(r)));
+    }
+  }
+#else
   fp6h t0;
   {
     const fp6h g0 = pld6(g, 0);
@@ -148,6 +184,7 @@ CESS_HD void pmul12(const S& f, const G& g) {
   CESS_MEMBAR();
   pst6(f, 1, sub(pld6(f, 0), t1));
   pst6(f, 0, add(t0, mul_v(t1)));
+#endif
 }
 
 // Fp6 square of the store half h (a pmul6 of the half with itself)

@@ -406,3 +406,22 @@ def test_loop_forms_keep_codes_and_gt(emu_loops, vectors, norm_pk):
                 assert bytes(gt).hex() == c["gt"], c["name"]
     finally:
         emu_loops.emu_set_norm_pk(old)
+
+
+def test_subfield_miller_value_degenerate_chain(emu):
+    """Secret keys 1 and r - 1 (key +-G2, signature +-H(m)): the Miller value
+    lies in Fp6, the easy part gives m = 1 and the hard part's compressed
+    powers are all zero -- the staged program's Granger-Scott fallback
+    (bls/staged.hpp cyc_chain) must still return Gt = 1, code 0, as the oracle
+    (and the value-based code) do (tests/test_gpu_subfield.py on the GPU)."""
+    import oracle.bls_oracle as o
+    one = o.gt_to_bytes(o.F12_ONE)
+    for msg in (b"", b"subfield miller value"):
+        h = o.hash_to_g1(msg)
+        for sig_pt, pk_pt in ((h, o.G2_GEN), (o.ec_neg(o.FP, h), o.ec_neg(o.FP2, o.G2_GEN))):
+            s, k = o.g1_to_compressed(sig_pt), o.g2_to_compressed(pk_pt)
+            g1 = (ctypes.c_uint8 * 576)()
+            g2 = (ctypes.c_uint8 * 576)()
+            assert emu.emu_verify(s, msg, len(msg), k, g1) == 0
+            assert emu.emu_gt_valuebased(s, msg, len(msg), k, g2) == 0
+            assert bytes(g1) == one and bytes(g2) == one

@@ -684,15 +684,23 @@ CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
 // f, g and to the Bezout coefficients d, e (mod p, exact division by 2^30 via a
 // multiple of p).  37 x 30 = 1,110 divsteps >= floor((49 d + 57) / 17) = 1,101
 // for d = 381 bits, the paper's bound (Theorem 11.2), so g reaches 0 for every
-// input.  Cost ~3 x 10^4 VALU instructions, about 40 Montgomery products,
-// against ~490 products (380 squarings + windowed multiplies) for a^(p-2).
+// input.  Since round 6 the steps are the half-delta variant (delta starts at
+// 1/2; libsecp256k1's safegcd analysis puts its worst case lower, ~880
+// divsteps for 381 bits, so the 37-iteration cap stays a safe bound), and the
+// loop leaves as soon as g = 0 in every lane of the wave: once g = 0 further
+// divsteps leave f and d unchanged, so the early exit is exact.  Random inputs
+// need 26-28 iterations (half-delta 26-27; 200,000 samples,
+// tools/divsteps_sim.c), not 37.  Cost ~1,240 VALU per iteration (~3.3 x 10^4
+// per inversion), about 60 Montgomery products, against ~490 for a^(p-2).
 struct s30 {
   int32_t v[13];
 };
 constexpr int32_t M30 = 0x3fffffff;
 
-// 30 divsteps (original, delta form; zeta = -delta, delta starts at 1) on the
-// low bits f0 (odd), g0; returns zeta and the matrix [u v; q r] with
+// 30 divsteps (half-delta form: zeta = -(delta + 1/2), delta starts at 1/2,
+// so zeta starts at -1; a swap step sets delta to 1 - delta, i.e. zeta to
+// -zeta - 2, any other step delta to 1 + delta, zeta to zeta - 1) on the low
+// bits f0 (odd), g0; returns zeta and the matrix [u v; q r] with
 // 2^30 [f'; g'] = [u v; q r] [f; g]
 CESS_HD int32_t divsteps30(int32_t zeta, uint32_t f, uint32_t g, int32_t& ou, int32_t& ov, int32_t& oq,
                            int32_t& orr) {
@@ -706,7 +714,7 @@ CESS_HD int32_t divsteps30(int32_t zeta, uint32_t f, uint32_t g, int32_t& ou, in
     q += y & c2;
     r += z & c2;
     c1 &= c2;   // swap step: delta > 0 and g odd
-    zeta = (int32_t)(((uint32_t)zeta ^ c1) - 1u - c1);   // swap: -zeta - 1, else zeta - 1
+    zeta = (int32_t)(((uint32_t)zeta ^ c1) - 1u);   // swap: -zeta - 2, else zeta - 1
     f += g & c1;
     u += q & c1;
     v += r & c1;
@@ -797,6 +805,16 @@ CESS_HD fp inv(const fp& a0) {
   int32_t zeta = -1;
 #pragma unroll 1
   for (int it = 0; it < 37; it++) {
+    if (it >= 25) {   // leave once g = 0 in every lane of the wave (uniform)
+      uint32_t nz = 0;
+#pragma unroll
+      for (int k = 0; k < 13; k++) nz |= (uint32_t)g.v[k];
+#if defined(CESS_HOSTEMU)
+      if (nz == 0) break;
+#else
+      if (__ballot(nz != 0) == 0) break;
+#endif
+    }
     int32_t u, v, q, r;
     zeta = divsteps30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], u, v, q, r);
     update_de30(d, e, u, v, q, r);

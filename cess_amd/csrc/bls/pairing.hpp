@@ -89,17 +89,34 @@ CESS_HD void g2_prepare(const fp2& qx, const fp2& qy, Sink&& sink, g2p* t = null
 // scratch) with the value-returning steps above and the key in registers.
 // Every multiply is sequenced (field.hpp seq), so the program order below is
 // the order the values are produced and die in.
+#ifndef CESS_DBL_SQR_XY
+#define CESS_DBL_SQR_XY 1
+#endif
 template <class Emit>
 CESS_HD void doubling_step_emit(g2p& r, int k, Emit&& emit) {
+#if CESS_DBL_SQR_XY
+  // 2XY = 4A as (X + Y)^2 - X^2 - Y^2: a squaring for a product (2M + 7S);
+  // X3 = 2 (2A)(B - F) = (4A)(B - F) below takes it without the doubling
+  const fp2 J = sqr(r.x);
+  emit(k, 1, neg(mul3(J)));                             // -3 X^2
+  const fp2 B = sqr(r.y);
+  const fp2 A4 = sub(sub(sqr(add(r.x, r.y)), J), B);    // 4A; X dead
+  const fp2 C = sqr(r.z);
+#else
   emit(k, 1, neg(mul3(sqr(r.x))));                      // -3 X^2
   const fp2 A2 = mul(r.x, r.y);                         // 2A; X dead
   const fp2 B = sqr(r.y), C = sqr(r.z);
+#endif
   const fp2 H = sub(sub(sqr(add(r.y, r.z)), B), C);     // 2YZ; Y, Z dead
   emit(k, 0, H);
   const fp2 E = mul3(mul4(mul_nr(C)));                  // 3 b' Z^2; C dead
   emit(k, 2, sub(B, E));
   const fp2 F = mul3(E);
+#if CESS_DBL_SQR_XY
+  const fp2 nx = mul(A4, sub(B, F));
+#else
   const fp2 nx = dbl(mul(A2, sub(B, F)));
+#endif
   const fp2 ny = sub(sqr(add(B, F)), mul4(mul3(sqr(E))));
   r = {nx, ny, mul4(mul(B, H))};
 }

@@ -628,6 +628,9 @@ CESS_HD uint32_t exp_bit(const uint32_t (&e)[12], int i) { return (e[i >> 5] >> 
 #ifndef CESS_POW_W
 #define CESS_POW_W 4
 #endif
+#ifndef CESS_POW_SWITCH
+#define CESS_POW_SWITCH 1
+#endif
 CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
   constexpr int W = CESS_POW_W, NT = 1 << (W - 1);   // odd powers a, a^3, .., a^(2^W - 1)
   fp a = a0;
@@ -656,6 +659,21 @@ CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
       v = 2 * v + exp_bit(e, k);
       if (started) sqr_d(r);
     }
+#if CESS_POW_SWITCH
+    // v is wave-uniform: a scalar branch to one copy of the table entry (14
+    // moves) instead of NT - 1 selects per digit
+#if defined(CESS_HOSTEMU)
+    const uint32_t m0 = v >> 1;
+#else
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(v >> 1);
+#endif
+#pragma unroll
+    for (int m = 0; m < NT; m++)
+      if (m0 == (uint32_t)m) {
+#pragma unroll
+        for (int q = 0; q < 14; q++) w[q] = t[m][q];
+      }
+#else
     // uniform selects (v is wave-uniform): no dynamically indexed table
 #pragma unroll
     for (int q = 0; q < 14; q++) {
@@ -664,6 +682,7 @@ CESS_HD fp pow_fixed(const fp& a0, const uint32_t (&e)[12]) {
       for (int m = 1; m < NT; m++) x = v == (uint32_t)(2 * m + 1) ? t[m][q] : x;
       w[q] = x;
     }
+#endif
     if (started) {
       mul_d(r, r, w);
     } else {

@@ -571,9 +571,9 @@ CESS_HD fp to_mont(const fp& a_raw) { return mul(a_raw, fp_from(c::R2)); }
 // a^e for a fixed 12-word exponent: MSB-first sliding window of width W
 // (CESS_POW_W, default 4: decode/hash kernels 1-3 % faster than width 3 on
 // one MI355X, width 5 spills -- profiles/round4_d_sweep.txt) over the odd
-// powers a, a^3, .., a^(2^W - 1) (table held in registers; the window is
-// picked with uniform selects, not a dynamically indexed array, so nothing goes
-// to scratch).  For the 379-381-bit exponents used here (p-2, (p+1)/4,
+// powers a, a^3, .., a^(2^W - 1) (table held in registers; the window's entry
+// is copied under a wave-uniform branch, CESS_POW_SWITCH, not read through a
+// dynamically indexed array, so nothing goes to scratch).  For the 379-381-bit exponents used here (p-2, (p+1)/4,
 // (p-3)/4; ~229 set bits) this is ~110 multiplies instead of ~229.  All
 // branches depend on the exponent only, so they are wave-uniform.
 // The chain runs in the 28-bit digit domain: a Montgomery product's digits

@@ -91,7 +91,10 @@ def test_staged_kernels_scratch_budget(tmp_path):
     assert final[0].get(".private_segment_fixed_size", 1 << 20) <= 1024, final
     # the SSWU values parked in LDS (bls/h2c.hpp hash_to_g1_parked): k_hash and
     # k_hash_out 304 -> 24 B/lane, k_sign 512 -> 384 (its GLV ladder spills the
-    # rest)
-    for name, cap in (("k_hash", 64), ("k_hash_out", 64), ("k_sign", 400)):
+    # rest).  Round 6: the uniform-branch window lookup of
+    # pow_fixed (CESS_POW_SWITCH) takes k_hash to 84 B -- every access outside
+    # the loops, one spill and reload around each powering, and the kernel
+    # 24.6 -> 24.3 ms (profiles/round6_an_sweep_pow_switch.txt)
+    for name, cap in (("k_hash", 96), ("k_hash_out", 96), ("k_sign", 400)):
         ks = [v for k, v in notes.items() if k.startswith("_Z%d%s" % (len(name), name))]
         assert ks and ks[0].get(".private_segment_fixed_size", 1 << 20) <= cap, (name, ks)

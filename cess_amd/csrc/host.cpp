@@ -114,7 +114,11 @@ static uint64_t launch_records(uint64_t cap) {
 // pipeline costs one lane's latency through six kernels whatever the batch
 // size.  Env CESS_BLS_SMALL_BATCH (0 disables).
 static uint64_t small_records() {
-  uint64_t v = 8192;   // measured (profiles/round3_*_latency.txt)
+  // measured crossover: with the round-6 lane-pair heavy kernels the pipeline
+  // takes 17.0-17.4 ms from 4,096 to 5,632 records against k_group's 13.7 /
+  // 16.2 / 18.7 ms at 4,096 / 5,120 / 5,632 (profiles/round6_ap_latency.txt,
+  // round6_aq_latency.txt; 8,192 in rounds 3-5, profiles/round3_*_latency.txt)
+  uint64_t v = 5120;
   if (const char* e = getenv("CESS_BLS_SMALL_BATCH")) v = strtoull(e, nullptr, 10);
   return v;
 }
